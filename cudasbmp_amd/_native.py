@@ -1,0 +1,135 @@
+"""ctypes binding of libsbmp.so (the C ABI in include/sbmp/sbmp.h).
+
+The product path has no CPU fallback: if the HIP library is missing or fails to
+load, every entry point raises NativeLibraryError.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+_PKG = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_PKG, "libsbmp.so")
+
+SBMP_OK = 0
+SBMP_AGENT_CAR = 0
+SBMP_AGENT_POINT = 1
+SBMP_COMM_ID_BYTES = 128
+
+
+class NativeLibraryError(RuntimeError):
+    pass
+
+
+class SbmpError(RuntimeError):
+    def __init__(self, status: int, func: str, msg: str):
+        super().__init__(f"{func} failed with status {status}: {msg}")
+        self.status = status
+
+
+class KgmtParams(ctypes.Structure):
+    _fields_ = [
+        ("width", ctypes.c_float), ("height", ctypes.c_float),
+        ("N", ctypes.c_int), ("n", ctypes.c_int),
+        ("numIterations", ctypes.c_int), ("maxTreeSize", ctypes.c_int), ("numDisc", ctypes.c_int),
+        ("agentLength", ctypes.c_float), ("goalThreshold", ctypes.c_float),
+        ("samplesPerIteration", ctypes.c_int), ("agent", ctypes.c_int), ("fixGNewClear", ctypes.c_int),
+        ("device", ctypes.c_int), ("profileKernels", ctypes.c_int),
+    ]
+
+
+class PlanResult(ctypes.Structure):
+    _fields_ = [
+        ("iterations", ctypes.c_int), ("treeSize", ctypes.c_int), ("costToGoal", ctypes.c_float),
+        ("goalIndex", ctypes.c_int), ("samplesGenerated", ctypes.c_longlong), ("accepted", ctypes.c_longlong),
+        ("wallMs", ctypes.c_double), ("stalled", ctypes.c_int),
+    ]
+
+
+ITER_FIELDS = ("itr", "treeSizeBefore", "nG", "k", "nExp", "S", "A", "treeSizeAfter", "goalIdx")
+
+
+class IterRecord(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int) for n in ITER_FIELDS]
+
+
+class KernelStat(ctypes.Structure):
+    _fields_ = [("name", ctypes.c_char * 32), ("launches", ctypes.c_longlong), ("totalMs", ctypes.c_double)]
+
+
+# Every symbol include/sbmp/sbmp.h declares (checked by tests/test_abi.py).
+EXPORTED_SYMBOLS = (
+    "sbmp_abi_version", "sbmp_status_string", "sbmp_last_error", "sbmp_kgmt_default_params",
+    "sbmp_kgmt_create", "sbmp_kgmt_destroy", "sbmp_kgmt_plan", "sbmp_kgmt_begin", "sbmp_kgmt_step",
+    "sbmp_kgmt_enqueue", "sbmp_kgmt_sync", "sbmp_kgmt_result", "sbmp_kgmt_stream", "sbmp_kgmt_copy_tree",
+    "sbmp_kgmt_copy_unexplored", "sbmp_kgmt_copy_flags", "sbmp_kgmt_copy_regions", "sbmp_kgmt_num_slots",
+    "sbmp_kgmt_copy_rng", "sbmp_kgmt_iter_log", "sbmp_kgmt_export_csv", "sbmp_kgmt_kernel_stats",
+    "sbmp_kgmt_reset_kernel_stats", "sbmp_read_obstacles_csv", "sbmp_device_upload_f32", "sbmp_device_free",
+    "sbmp_device_count", "sbmp_comm_get_unique_id", "sbmp_kgmt_create_sharded",
+)
+
+_lib = None
+
+
+def lib():
+    """Load libsbmp.so (once).  Raises NativeLibraryError if it is absent."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise NativeLibraryError(
+            f"{LIB_PATH} not found: build it with `python -m cudasbmp_amd.build` (hipcc, gfx950). "
+            "There is no CPU fallback for the planner.")
+    try:
+        L = ctypes.CDLL(LIB_PATH)
+    except OSError as e:
+        raise NativeLibraryError(f"failed to load {LIB_PATH}: {e}") from e
+    vp, i, P = ctypes.c_void_p, ctypes.c_int, ctypes.POINTER
+    L.sbmp_abi_version.restype = i
+    L.sbmp_status_string.restype = ctypes.c_char_p
+    L.sbmp_status_string.argtypes = [i]
+    L.sbmp_last_error.restype = ctypes.c_char_p
+    sig = {
+        "sbmp_kgmt_default_params": [P(KgmtParams)],
+        "sbmp_kgmt_create": [P(KgmtParams), P(vp)],
+        "sbmp_kgmt_create_sharded": [P(KgmtParams), vp, i, i, P(vp)],
+        "sbmp_comm_get_unique_id": [vp],
+        "sbmp_kgmt_destroy": [vp],
+        "sbmp_kgmt_plan": [vp, vp, vp, vp, i, ctypes.c_uint64, P(PlanResult)],
+        "sbmp_kgmt_begin": [vp, vp, vp, vp, i, ctypes.c_uint64],
+        "sbmp_kgmt_step": [vp, i, P(i)],
+        "sbmp_kgmt_enqueue": [vp, i],
+        "sbmp_kgmt_sync": [vp],
+        "sbmp_kgmt_result": [vp, P(PlanResult)],
+        "sbmp_kgmt_stream": [vp, P(vp)],
+        "sbmp_kgmt_copy_tree": [vp, vp, vp, vp, i],
+        "sbmp_kgmt_copy_unexplored": [vp, vp, vp, i],
+        "sbmp_kgmt_copy_flags": [vp, vp, vp, i],
+        "sbmp_kgmt_copy_regions": [vp] * 9,
+        "sbmp_kgmt_num_slots": [vp, P(i)],
+        "sbmp_kgmt_copy_rng": [vp, vp, i],
+        "sbmp_kgmt_iter_log": [vp, vp, i, P(i)],
+        "sbmp_kgmt_export_csv": [vp, ctypes.c_char_p],
+        "sbmp_kgmt_kernel_stats": [vp, vp, i, P(i)],
+        "sbmp_kgmt_reset_kernel_stats": [vp],
+        "sbmp_read_obstacles_csv": [ctypes.c_char_p, i, vp, i, P(i)],
+        "sbmp_device_upload_f32": [vp, ctypes.c_size_t, P(vp)],
+        "sbmp_device_free": [vp],
+        "sbmp_device_count": [P(i)],
+    }
+    for name, args in sig.items():
+        f = getattr(L, name)
+        f.argtypes = args
+        f.restype = i
+    _lib = L
+    return _lib
+
+
+def check(status: int, func: str) -> None:
+    if status != SBMP_OK:
+        msg = lib().sbmp_last_error().decode(errors="replace")
+        raise SbmpError(status, func, msg)
+
+
+def call(name: str, *args) -> None:
+    check(getattr(lib(), name)(*args), name)

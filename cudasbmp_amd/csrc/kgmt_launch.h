@@ -1,0 +1,29 @@
+// kgmt_launch.h — host-side launch entry points of kgmt_kernels.hip.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <vector>
+
+#include "kgmt_device.h"
+
+namespace sbmp {
+
+void launch_expand(const KgmtDev& d, int t, int agent, int blocks, hipStream_t s);
+void launch_plan(const KgmtDev& d, int t, hipStream_t s);
+void launch_insert(const KgmtDev& d, int t, int blocks, hipStream_t s);
+void launch_fill_i32(int* p, int v, long long n, hipStream_t s);
+void launch_fill_f32(float* p, float v, long long n, hipStream_t s);
+void launch_init_slots(const KgmtDev& d, const Xorwow& base, const uint32_t* jumps, int nbits, int blocks,
+                       hipStream_t s);
+void launch_seed_root(const KgmtDev& d, float4 rs, float4 rc, int r1, int r2, hipStream_t s);
+void launch_export_tree(const KgmtDev& d, float* samples, float* costs, hipStream_t s);
+void launch_export_unexplored(const KgmtDev& d, float* samples, int* uParent, hipStream_t s);
+
+// xorwow_jump.cpp: cuRAND seeding and the subsequence jump matrices.
+Xorwow curand_seed_state(uint64_t seed);
+// J[b] = A^(2^(67+b)), b < nbits, each 160 columns x 5 words, concatenated.
+const std::vector<uint32_t>& subsequence_jump_matrices(int nbits);
+
+}  // namespace sbmp

@@ -1,0 +1,514 @@
+// kgmt_planner.cpp — host driver of the device-resident KGMT loop.
+//
+// Reference: KGMT::KGMT (src/planners/KGMT.cu:10-78) allocates ~25 thrust vectors;
+// KGMT::plan (KGMT.cu:80-317) runs a host loop with >= 6 blocking device->host
+// reads per iteration.  Here every iteration is three kernels whose sizes live
+// in device memory (IterCtrl), so the host only enqueues; it synchronises once
+// per `pollEvery` iterations to learn whether the loop has ended.
+#include "kgmt_planner.h"
+
+#include <algorithm>
+#include <chrono>
+#include <cstring>
+#include <fstream>
+#include <iomanip>
+#include <sys/stat.h>
+
+#include "kgmt_launch.h"
+
+namespace sbmp {
+
+double now_ms() {
+    using namespace std::chrono;
+    return duration<double, std::milli>(steady_clock::now().time_since_epoch()).count();
+}
+
+template <typename T>
+T* KgmtPlanner::alloc(size_t n) {
+    void* p = nullptr;
+    const size_t bytes = std::max<size_t>(n, 1) * sizeof(T);
+    hipError_t e = hipMalloc(&p, bytes);
+    if (e != hipSuccess)
+        throw Error(e == hipErrorOutOfMemory ? SBMP_ERR_OUT_OF_MEMORY : SBMP_ERR_HIP,
+                    "hipMalloc(" + std::to_string(bytes) + "): " + hipGetErrorString(e));
+    allocs_.push_back(p);
+    return static_cast<T*>(p);
+}
+
+static int round_up(long long x, long long m) { return (int)(((x + m - 1) / m) * m); }
+
+KgmtPlanner::KgmtPlanner(const sbmp_kgmt_params& p, int nranks, int rank, Exchange* ex) : p_(p), ex_(ex) {
+    if (p.N * p.N != kMaxR1) throw Error(SBMP_ERR_INVALID_ARGUMENT, "N must be 16 (reference KGMT.cu:8 NUM_R1)");
+    if (p.n < 1 || p.n > 16) throw Error(SBMP_ERR_INVALID_ARGUMENT, "n must be in [1, 16]");
+    if (p.maxTreeSize < 1) throw Error(SBMP_ERR_INVALID_ARGUMENT, "maxTreeSize must be >= 1");
+    if (p.numDisc < 1) throw Error(SBMP_ERR_INVALID_ARGUMENT, "numDisc must be >= 1");
+    if (p.numIterations < 0) throw Error(SBMP_ERR_INVALID_ARGUMENT, "numIterations must be >= 0");
+    if (p.samplesPerIteration < 0) throw Error(SBMP_ERR_INVALID_ARGUMENT, "samplesPerIteration must be >= 0");
+    if (p.agent != SBMP_AGENT_CAR && p.agent != SBMP_AGENT_POINT) throw Error(SBMP_ERR_INVALID_ARGUMENT, "unknown agent");
+    if (!(p.width > 0.0f) || !(p.height > 0.0f)) throw Error(SBMP_ERR_INVALID_ARGUMENT, "width/height must be > 0");
+    if (nranks < 1 || rank < 0 || rank >= nranks) throw Error(SBMP_ERR_INVALID_ARGUMENT, "bad rank/nranks");
+    int ndev = 0;
+    SBMP_HIP(hipGetDeviceCount(&ndev));
+    if (p.device < 0 || p.device >= ndev) throw Error(SBMP_ERR_INVALID_ARGUMENT, "no such HIP device");
+    SBMP_HIP(hipSetDevice(p.device));
+    SBMP_HIP(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+
+    const int M = p.maxTreeSize;
+    const int nSlots = p.samplesPerIteration > 0 ? std::min(M, p.samplesPerIteration) : M;
+    slotsPadded_ = round_up(nSlots, (long long)kBlock * nranks);
+    expandBlocks_ = slotsPadded_ / kBlock / nranks;
+    const int nWords = slotsPadded_ / kWave;
+    insertBlocks_ = (nWords + (kBlock / kWave) - 1) / (kBlock / kWave);
+    while ((1ll << nbits_) < nSlots) ++nbits_;
+
+    KgmtDev& d = d_;
+    d.M = M;
+    d.nSlots = nSlots;
+    d.nWords = nWords;
+    d.numIterations = p.numIterations;
+    d.numDisc = p.numDisc;
+    d.N = p.N;
+    d.n = p.n;
+    d.nR1 = p.N * p.N;
+    d.nR2 = d.nR1 * p.n * p.n;
+    d.cap = p.samplesPerIteration;
+    d.fixGNewClear = p.fixGNewClear;
+    d.nranks = nranks;
+    d.rank = rank;
+    d.width = p.width;
+    d.height = p.height;
+    d.agentLength = p.agentLength;
+    d.goalThreshold = p.goalThreshold;
+    d.R1Size = p.width / (float)p.N;          // KGMT.cu:13
+    d.R2Size = p.width / (float)(p.n * p.N);  // KGMT.cu:14
+
+    d.treeState = alloc<float4>(M);
+    d.treeCtrl = alloc<float4>(M);
+    d.treeParent = alloc<int>(M);
+    d.uState = alloc<float4>(slotsPadded_);
+    d.uCtrl = alloc<float4>(slotsPadded_);
+    d.rngA = alloc<uint4>(slotsPadded_);
+    d.rngB = alloc<uint2>(slotsPadded_);
+    d.gnew = alloc<unsigned long long>(nWords);
+    d.wordOffsets = alloc<int>(nWords);
+    d.R1 = alloc<int>(d.nR1);
+    d.R1Avail = alloc<int>(d.nR1);
+    d.R1Valid = alloc<int>(d.nR1);
+    d.R1Invalid = alloc<int>(d.nR1);
+    d.R1Cov = alloc<int>(d.nR1);
+    d.R2Avail = alloc<uint32_t>(d.nR2 / 32);
+    d.R2Snap = alloc<uint32_t>(d.nR2 / 32);
+    d.R2Valid = alloc<int>(d.nR2);
+    d.R2Invalid = alloc<int>(d.nR2);
+    d.R1Score = alloc<float>(2 * d.nR1);
+    d.delta = alloc<int>(4 * d.nR1 + d.nR2);
+    d.ctrl = alloc<IterCtrl>(p.numIterations + 2);
+    d.status = alloc<PlannerStatus>(1);
+    jumps_ = alloc<uint32_t>((size_t)nbits_ * 800);
+    const std::vector<uint32_t>& J = subsequence_jump_matrices(nbits_);
+    SBMP_HIP(hipMemcpyAsync(jumps_, J.data(), (size_t)nbits_ * 800 * sizeof(uint32_t), hipMemcpyHostToDevice,
+                            stream_));
+    SBMP_HIP(hipStreamSynchronize(stream_));
+}
+
+KgmtPlanner::~KgmtPlanner() {
+    if (stream_) {
+        (void)hipSetDevice(p_.device);
+        (void)hipStreamSynchronize(stream_);
+    }
+    for (auto& q : pending_) {
+        (void)hipEventDestroy(q.a);
+        (void)hipEventDestroy(q.b);
+    }
+    for (hipEvent_t e : eventPool_) (void)hipEventDestroy(e);
+    for (void* ptr : allocs_) (void)hipFree(ptr);
+    if (obs_) (void)hipFree(obs_);
+    if (stream_) (void)hipStreamDestroy(stream_);
+}
+
+void KgmtPlanner::begin(const float* initial, const float* goal, const float* d_obstacles, int nObs, uint64_t seed) {
+    if (!initial || !goal) throw Error(SBMP_ERR_INVALID_ARGUMENT, "initial/goal must be non-NULL");
+    if (nObs < 0 || (nObs > 0 && !d_obstacles)) throw Error(SBMP_ERR_INVALID_ARGUMENT, "bad obstacles");
+    SBMP_HIP(hipSetDevice(p_.device));
+    KgmtDev& d = d_;
+    hipStream_t s = stream_;
+    // Constructor state (KGMT.cu:16-72): zero-filled vectors, parents -1, R1Score 1.0.
+    SBMP_HIP(hipMemsetAsync(d.treeState, 0, sizeof(float4) * d.M, s));
+    SBMP_HIP(hipMemsetAsync(d.treeCtrl, 0, sizeof(float4) * d.M, s));
+    launch_fill_i32(d.treeParent, -1, d.M, s);
+    SBMP_HIP(hipMemsetAsync(d.gnew, 0, sizeof(unsigned long long) * d.nWords, s));
+    SBMP_HIP(hipMemsetAsync(d.wordOffsets, 0, sizeof(int) * d.nWords, s));
+    for (int* a : {d.R1, d.R1Avail, d.R1Valid, d.R1Invalid, d.R1Cov})
+        SBMP_HIP(hipMemsetAsync(a, 0, sizeof(int) * d.nR1, s));
+    SBMP_HIP(hipMemsetAsync(d.R2Avail, 0, sizeof(uint32_t) * (d.nR2 / 32), s));
+    SBMP_HIP(hipMemsetAsync(d.R2Snap, 0, sizeof(uint32_t) * (d.nR2 / 32), s));
+    SBMP_HIP(hipMemsetAsync(d.R2Valid, 0, sizeof(int) * d.nR2, s));
+    SBMP_HIP(hipMemsetAsync(d.R2Invalid, 0, sizeof(int) * d.nR2, s));
+    launch_fill_f32(d.R1Score, 1.0f, 2 * d.nR1, s);
+    SBMP_HIP(hipMemsetAsync(d.delta, 0, sizeof(int) * (4 * d.nR1 + d.nR2), s));
+    SBMP_HIP(hipMemsetAsync(d.ctrl, 0, sizeof(IterCtrl) * (p_.numIterations + 2), s));
+
+    // Obstacles: a private float4 copy of the caller's device array (KGMT.cu:80 takes
+    // d_obstacles by pointer; copying keeps the row layout 16-B aligned).
+    if (nObs > obsCap_) {
+        if (obs_) SBMP_HIP(hipFree(obs_));
+        obs_ = nullptr;
+        SBMP_HIP(hipMalloc(&obs_, sizeof(float4) * nObs));
+        obsCap_ = nObs;
+    }
+    if (nObs > 0)
+        SBMP_HIP(hipMemcpyAsync(obs_, d_obstacles, sizeof(float4) * nObs, hipMemcpyDeviceToDevice, s));
+    d.obstacles = obs_;
+    d.nObs = nObs;
+    d.goalX = goal[0];
+    d.goalY = goal[1];
+
+    // Root (KGMT.cu:85-97).
+    const int r1 = getR1(initial[0], initial[1], d.R1Size, d.N);
+    const int r2 = getR2(initial[0], initial[1], r1, d.R1Size, d.N, d.R2Size, d.n);
+    launch_seed_root(d, make_float4(initial[0], initial[1], initial[2], initial[3]),
+                     make_float4(initial[4], initial[5], initial[6], 0.0f), r1, r2, s);
+    // curand_init(seed, slot, 0) for every slot (KGMT.cu:109-111, D1).
+    launch_init_slots(d, curand_seed_state(seed), jumps_, nbits_, expandBlocks_, s);
+    SBMP_HIP(hipGetLastError());
+
+    t_next_ = 1;
+    begun_ = true;
+    wallMs_ = 0.0;
+    SBMP_HIP(hipStreamSynchronize(s));
+    t0_ = now_ms();
+    timed_begin(K_PLAN);
+    launch_plan(d, 1, s);
+    timed_end(K_PLAN);
+    SBMP_HIP(hipGetLastError());
+}
+
+void KgmtPlanner::enqueue(int iterations) {
+    if (!begun_) throw Error(SBMP_ERR_STATE, "begin() has not been called");
+    for (int i = 0; i < iterations && t_next_ <= p_.numIterations; ++i) {
+        const int t = t_next_++;
+        if (d_.nranks > 1) {
+            enqueue_sharded_iteration(t);
+            continue;
+        }
+        timed_begin(K_EXPAND);
+        launch_expand(d_, t, p_.agent, expandBlocks_, stream_);
+        timed_end(K_EXPAND);
+        timed_begin(K_PLAN);
+        launch_plan(d_, t + 1, stream_);
+        timed_end(K_PLAN);
+        timed_begin(K_INSERT);
+        launch_insert(d_, t, insertBlocks_, stream_);
+        timed_end(K_INSERT);
+    }
+    SBMP_HIP(hipGetLastError());
+}
+
+void KgmtPlanner::sync() {
+    SBMP_HIP(hipStreamSynchronize(stream_));
+    wallMs_ = now_ms() - t0_;
+}
+
+void KgmtPlanner::read_ctrl(std::vector<IterCtrl>& c, PlannerStatus& st) {
+    c.resize(p_.numIterations + 2);
+    SBMP_HIP(hipMemcpyAsync(c.data(), d_.ctrl, sizeof(IterCtrl) * c.size(), hipMemcpyDeviceToHost, stream_));
+    SBMP_HIP(hipMemcpyAsync(&st, d_.status, sizeof(PlannerStatus), hipMemcpyDeviceToHost, stream_));
+    SBMP_HIP(hipStreamSynchronize(stream_));
+}
+
+int KgmtPlanner::last_executed(const std::vector<IterCtrl>& c) const {
+    int itr = 0;
+    for (int t = 1; t < t_next_ && t < (int)c.size(); ++t) {
+        if (c[t].executed) itr = t;
+        else break;
+    }
+    return itr;
+}
+
+bool KgmtPlanner::active() {
+    if (!begun_) return false;
+    sync();
+    if (t_next_ > p_.numIterations) return false;
+    IterCtrl c;
+    PlannerStatus st;
+    SBMP_HIP(hipMemcpy(&c, d_.ctrl + t_next_, sizeof(IterCtrl), hipMemcpyDeviceToHost));
+    SBMP_HIP(hipMemcpy(&st, d_.status, sizeof(PlannerStatus), hipMemcpyDeviceToHost));
+    // ctrl[t_next] was written by the last enqueued plan kernel: it says whether the
+    // next iteration would run (tree not full, limit not reached); the goal ends it too.
+    return c.run && st.goalIdx == kNoGoal;
+}
+
+void KgmtPlanner::run(int pollEvery) {
+    if (pollEvery < 1) pollEvery = 1;
+    while (true) {
+        enqueue(pollEvery);
+        if (!active()) break;
+    }
+    sync();
+}
+
+void KgmtPlanner::result(sbmp_plan_result* r) {
+    sync();
+    std::vector<IterCtrl> c;
+    PlannerStatus st;
+    read_ctrl(c, st);
+    const int itr = last_executed(c);
+    memset(r, 0, sizeof(*r));
+    r->iterations = itr;
+    r->treeSize = itr > 0 ? c[itr].treeSize + c[itr].A : 1;
+    for (int t = 1; t <= itr; ++t) {
+        r->samplesGenerated += c[t].S;
+        r->accepted += c[t].A;
+    }
+    r->goalIndex = (st.goalIdx == kNoGoal) ? -1 : st.goalIdx;
+    r->costToGoal = 0.0f;
+    if (r->goalIndex >= 0) {
+        float4 gc;
+        SBMP_HIP(hipMemcpy(&gc, d_.treeCtrl + r->goalIndex, sizeof(float4), hipMemcpyDeviceToHost));
+        r->costToGoal = gc.w;
+    }
+    r->wallMs = wallMs_;
+    r->stalled = (itr > 0 && c[itr].nG == 0) ? 1 : 0;
+}
+
+std::vector<sbmp_iter_record> KgmtPlanner::iter_log() {
+    sync();
+    std::vector<IterCtrl> c;
+    PlannerStatus st;
+    read_ctrl(c, st);
+    const int itr = last_executed(c);
+    std::vector<sbmp_iter_record> out;
+    for (int t = 1; t <= itr; ++t) {
+        sbmp_iter_record e;
+        e.itr = t;
+        e.treeSizeBefore = c[t].treeSize;
+        e.nG = c[t].nG;
+        e.k = c[t].k;
+        e.nExp = c[t].nExp;
+        e.S = c[t].S;
+        e.A = c[t].A;
+        e.treeSizeAfter = c[t].treeSize + c[t].A;
+        e.goalIdx = (t == itr && st.goalIdx != kNoGoal) ? st.goalIdx : -1;
+        out.push_back(e);
+    }
+    return out;
+}
+
+void KgmtPlanner::copy_tree(float* samples, int* parent, float* costs) {
+    sync();
+    const size_t M = d_.M;
+    float* dS = nullptr;
+    float* dC = nullptr;
+    SBMP_HIP(hipMalloc(&dS, sizeof(float) * M * 7));
+    SBMP_HIP(hipMalloc(&dC, sizeof(float) * M));
+    launch_export_tree(d_, dS, dC, stream_);
+    if (samples) SBMP_HIP(hipMemcpyAsync(samples, dS, sizeof(float) * M * 7, hipMemcpyDeviceToHost, stream_));
+    if (costs) SBMP_HIP(hipMemcpyAsync(costs, dC, sizeof(float) * M, hipMemcpyDeviceToHost, stream_));
+    if (parent) SBMP_HIP(hipMemcpyAsync(parent, d_.treeParent, sizeof(int) * M, hipMemcpyDeviceToHost, stream_));
+    SBMP_HIP(hipStreamSynchronize(stream_));
+    (void)hipFree(dS);
+    (void)hipFree(dC);
+}
+
+void KgmtPlanner::copy_unexplored(float* samples, int* uParent) {
+    sync();
+    const size_t M = d_.M, n = d_.nSlots;
+    float* dS = nullptr;
+    int* dP = nullptr;
+    SBMP_HIP(hipMalloc(&dS, sizeof(float) * n * 7));
+    SBMP_HIP(hipMalloc(&dP, sizeof(int) * n));
+    launch_export_unexplored(d_, dS, dP, stream_);
+    // The reference's unexplored buffer has M rows; slots never used stay 0 / -1.
+    std::vector<float> hs(n * 7);
+    std::vector<int> hp(n);
+    SBMP_HIP(hipMemcpyAsync(hs.data(), dS, sizeof(float) * n * 7, hipMemcpyDeviceToHost, stream_));
+    SBMP_HIP(hipMemcpyAsync(hp.data(), dP, sizeof(int) * n, hipMemcpyDeviceToHost, stream_));
+    SBMP_HIP(hipStreamSynchronize(stream_));
+    (void)hipFree(dS);
+    (void)hipFree(dP);
+    if (d_.nranks > 1) {   // rows of slots owned by other ranks are not held here
+        for (size_t i = 0; i < n; ++i) {
+            if ((int)((i / kBlock) % d_.nranks) != d_.rank) {
+                for (int q = 0; q < 7; ++q) hs[i * 7 + q] = 0.0f;
+                hp[i] = -1;
+            }
+        }
+    }
+    if (samples) {
+        memcpy(samples, hs.data(), sizeof(float) * n * 7);
+        memset(samples + n * 7, 0, sizeof(float) * (M - n) * 7);
+    }
+    if (uParent) {
+        memcpy(uParent, hp.data(), sizeof(int) * n);
+        for (size_t i = n; i < M; ++i) uParent[i] = -1;
+    }
+}
+
+void KgmtPlanner::copy_flags(uint8_t* G, uint8_t* GNew) {
+    sync();
+    std::vector<IterCtrl> c;
+    PlannerStatus st;
+    read_ctrl(c, st);
+    const int itr = last_executed(c);
+    const int M = d_.M;
+    if (G) {
+        memset(G, 0, M);
+        int lo = 0, hi = 1;
+        if (itr > 0) {
+            lo = c[itr].gLo + c[itr].nExp;
+            hi = c[itr].treeSize + c[itr].A;
+        }
+        for (int i = lo; i < std::min(hi, M); ++i) G[i] = 1;
+    }
+    if (GNew) {
+        std::vector<unsigned long long> w(d_.nWords);
+        SBMP_HIP(hipMemcpy(w.data(), d_.gnew, sizeof(unsigned long long) * d_.nWords, hipMemcpyDeviceToHost));
+        memset(GNew, 0, M);
+        for (int s = 0; s < d_.nSlots; ++s) GNew[s] = (w[s >> 6] >> (s & 63)) & 1ull;
+    }
+}
+
+void KgmtPlanner::copy_regions(int* R1, int* R1Avail, int* R1Valid, int* R1Invalid, float* R1Score, int* R2Avail,
+                               int* R2Valid, int* R2Invalid) {
+    sync();
+    std::vector<IterCtrl> c;
+    PlannerStatus st;
+    read_ctrl(c, st);
+    const int itr = last_executed(c);
+    const size_t n1 = d_.nR1, n2 = d_.nR2;
+    auto cp = [&](void* dst, const void* src, size_t bytes) {
+        if (dst) SBMP_HIP(hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost));
+    };
+    cp(R1, d_.R1, sizeof(int) * n1);
+    cp(R1Avail, d_.R1Avail, sizeof(int) * n1);
+    cp(R1Valid, d_.R1Valid, sizeof(int) * n1);
+    cp(R1Invalid, d_.R1Invalid, sizeof(int) * n1);
+    cp(R1Score, d_.R1Score + (itr & 1) * n1, sizeof(float) * n1);
+    cp(R2Valid, d_.R2Valid, sizeof(int) * n2);
+    cp(R2Invalid, d_.R2Invalid, sizeof(int) * n2);
+    if (R2Avail) {
+        std::vector<uint32_t> bits(n2 / 32);
+        SBMP_HIP(hipMemcpy(bits.data(), d_.R2Avail, sizeof(uint32_t) * bits.size(), hipMemcpyDeviceToHost));
+        for (size_t i = 0; i < n2; ++i) R2Avail[i] = (bits[i >> 5] >> (i & 31)) & 1u;
+    }
+}
+
+void KgmtPlanner::copy_rng(uint32_t* states) {
+    sync();
+    const size_t n = d_.nSlots;
+    std::vector<uint4> a(n);
+    std::vector<uint2> b(n);
+    SBMP_HIP(hipMemcpy(a.data(), d_.rngA, sizeof(uint4) * n, hipMemcpyDeviceToHost));
+    SBMP_HIP(hipMemcpy(b.data(), d_.rngB, sizeof(uint2) * n, hipMemcpyDeviceToHost));
+    for (size_t i = 0; i < n; ++i) {
+        uint32_t* o = states + 6 * i;
+        o[0] = a[i].x;
+        o[1] = a[i].y;
+        o[2] = a[i].z;
+        o[3] = a[i].w;
+        o[4] = b[i].x;
+        o[5] = b[i].y;
+    }
+}
+
+// KGMT.cu:299-311 with helper.cuh:53-79 formatting.
+template <typename T>
+static void write_csv(const std::string& path, const T* v, size_t rows, size_t cols) {
+    std::ofstream f(path);
+    if (!f.is_open()) throw Error(SBMP_ERR_IO, "cannot open " + path);
+    f << std::fixed << std::setprecision(10);
+    for (size_t i = 0; i < rows; ++i) {
+        for (size_t j = 0; j < cols; ++j) {
+            f << v[i * cols + j];
+            if (j < cols - 1) f << ",";
+        }
+        f << std::endl;
+    }
+}
+
+void KgmtPlanner::export_csv(const std::string& dir) {
+    const size_t M = d_.M, n1 = d_.nR1, n2 = d_.nR2;
+    mkdir(dir.c_str(), 0755);
+    const std::string pre = dir.empty() ? "" : dir + "/";
+    std::vector<float> samples(M * 7), costs(M), uS(M * 7), score(n1);
+    std::vector<int> parent(M), uP(M), R1(n1), R1A(n1), R1V(n1), R1I(n1), R2A(n2), R2V(n2), R2I(n2);
+    std::vector<uint8_t> G(M), GN(M);
+    copy_tree(samples.data(), parent.data(), costs.data());
+    copy_unexplored(uS.data(), uP.data());
+    copy_flags(G.data(), GN.data());
+    copy_regions(R1.data(), R1A.data(), R1V.data(), R1I.data(), score.data(), R2A.data(), R2V.data(), R2I.data());
+    std::vector<int> Gi(G.begin(), G.end());
+    write_csv(pre + "samples.csv", samples.data(), M, 7);
+    write_csv(pre + "unexploredSamples.csv", uS.data(), M, 7);
+    write_csv(pre + "parentRelations.csv", parent.data(), M, 1);
+    write_csv(pre + "uParentIdx.csv", uP.data(), M, 1);
+    write_csv(pre + "G.csv", Gi.data(), M, 1);
+    write_csv(pre + "R2Avail.csv", R2A.data(), n2, 1);
+    write_csv(pre + "R1Avail.csv", R1A.data(), n1, 1);
+    write_csv(pre + "R1Valid.csv", R1V.data(), n1, 1);
+    write_csv(pre + "R2Valid.csv", R2V.data(), n2, 1);
+    write_csv(pre + "R1Invalid.csv", R1I.data(), n1, 1);
+    write_csv(pre + "R2Invalid.csv", R2I.data(), n2, 1);
+    write_csv(pre + "R1Score.csv", score.data(), n1, 1);
+    write_csv(pre + "R1.csv", R1.data(), n1, 1);
+}
+
+// ---------------------------------------------------------------- profiling
+void KgmtPlanner::timed_begin(int id) {
+    if (!p_.profileKernels) return;
+    hipEvent_t a, b;
+    for (hipEvent_t* e : {&a, &b}) {
+        if (!eventPool_.empty()) {
+            *e = eventPool_.back();
+            eventPool_.pop_back();
+        } else {
+            SBMP_HIP(hipEventCreate(e));
+        }
+    }
+    pending_.push_back({id, a, b});
+    SBMP_HIP(hipEventRecord(a, stream_));
+}
+
+void KgmtPlanner::timed_end(int id) {
+    if (!p_.profileKernels) return;
+    (void)id;
+    SBMP_HIP(hipEventRecord(pending_.back().b, stream_));
+}
+
+void KgmtPlanner::collect_events() {
+    for (auto& q : pending_) {
+        SBMP_HIP(hipEventSynchronize(q.b));
+        float ms = 0.0f;
+        SBMP_HIP(hipEventElapsedTime(&ms, q.a, q.b));
+        launches_[q.id] += 1;
+        totalMs_[q.id] += ms;
+        eventPool_.push_back(q.a);
+        eventPool_.push_back(q.b);
+    }
+    pending_.clear();
+}
+
+std::vector<sbmp_kernel_stat> KgmtPlanner::kernel_stats() {
+    collect_events();
+    static const char* names[K_COUNT] = {"k_expand", "k_plan", "k_insert", "k_pack", "k_merge_insert"};
+    std::vector<sbmp_kernel_stat> out;
+    for (int i = 0; i < K_COUNT; ++i) {
+        sbmp_kernel_stat s;
+        memset(&s, 0, sizeof(s));
+        strncpy(s.name, names[i], sizeof(s.name) - 1);
+        s.launches = launches_[i];
+        s.totalMs = totalMs_[i];
+        out.push_back(s);
+    }
+    return out;
+}
+
+void KgmtPlanner::reset_kernel_stats() {
+    collect_events();
+    for (int i = 0; i < K_COUNT; ++i) {
+        launches_[i] = 0;
+        totalMs_[i] = 0.0;
+    }
+}
+
+}  // namespace sbmp

@@ -1,0 +1,354 @@
+// sbmp_abi.cpp — extern "C" boundary of libsbmp.so (declared in include/sbmp/sbmp.h).
+// Every entry point converts exceptions into sbmp_status + a thread-local message.
+#include <cstdio>
+#include <cstring>
+#include <fstream>
+#include <sstream>
+#include <string>
+#include <vector>
+
+#include "kgmt_planner.h"
+#include "sbmp/sbmp.h"
+
+using sbmp::Error;
+using sbmp::KgmtPlanner;
+
+struct sbmp_kgmt {
+    KgmtPlanner* planner = nullptr;
+    void* comm = nullptr;   // sharded: owned collective context (kgmt_sharded.cpp)
+};
+
+namespace sbmp {
+void* sharded_create_comm(const uint8_t* id, int nranks, int rank, int device);
+void sharded_destroy_comm(void* comm);
+Exchange* sharded_exchange(void* comm);
+void comm_get_unique_id(uint8_t* id);
+}  // namespace sbmp
+
+static thread_local std::string g_last_error;
+
+template <typename F>
+static sbmp_status guarded(F&& f) {
+    try {
+        f();
+        return SBMP_OK;
+    } catch (const Error& e) {
+        g_last_error = e.what();
+        return e.status;
+    } catch (const std::bad_alloc&) {
+        g_last_error = "host out of memory";
+        return SBMP_ERR_OUT_OF_MEMORY;
+    } catch (const std::exception& e) {
+        g_last_error = e.what();
+        return SBMP_ERR_STATE;
+    }
+}
+
+#define REQUIRE(cond, msg)                                                   \
+    do {                                                                     \
+        if (!(cond)) throw Error(SBMP_ERR_INVALID_ARGUMENT, msg);            \
+    } while (0)
+
+extern "C" {
+
+int sbmp_abi_version(void) { return SBMP_ABI_VERSION; }
+
+const char* sbmp_status_string(sbmp_status s) {
+    switch (s) {
+        case SBMP_OK: return "ok";
+        case SBMP_ERR_INVALID_ARGUMENT: return "invalid argument";
+        case SBMP_ERR_HIP: return "HIP runtime error";
+        case SBMP_ERR_IO: return "I/O error";
+        case SBMP_ERR_OUT_OF_MEMORY: return "out of memory";
+        case SBMP_ERR_STATE: return "invalid state";
+        case SBMP_ERR_UNSUPPORTED: return "unsupported";
+        case SBMP_ERR_COMM: return "communication error";
+        default: return "unknown status";
+    }
+}
+
+const char* sbmp_last_error(void) { return g_last_error.c_str(); }
+
+sbmp_status sbmp_kgmt_default_params(sbmp_kgmt_params* p) {
+    return guarded([&] {
+        REQUIRE(p, "params is NULL");
+        memset(p, 0, sizeof(*p));
+        // reference demos/main.cu:19-28
+        p->width = 20.0f;
+        p->height = 20.0f;
+        p->N = 16;
+        p->n = 8;
+        p->numIterations = 100;
+        p->maxTreeSize = 30000;
+        p->numDisc = 10;
+        p->agentLength = 1.0f;
+        p->goalThreshold = 0.5f;
+        p->samplesPerIteration = 0;
+        p->agent = SBMP_AGENT_CAR;
+        p->fixGNewClear = 0;
+        p->device = 0;
+        p->profileKernels = 0;
+    });
+}
+
+sbmp_status sbmp_kgmt_create(const sbmp_kgmt_params* p, sbmp_kgmt** out) {
+    return guarded([&] {
+        REQUIRE(p && out, "NULL argument");
+        *out = nullptr;
+        sbmp_kgmt* h = new sbmp_kgmt;
+        try {
+            h->planner = new KgmtPlanner(*p);
+        } catch (...) {
+            delete h;
+            throw;
+        }
+        *out = h;
+    });
+}
+
+sbmp_status sbmp_kgmt_create_sharded(const sbmp_kgmt_params* p, const uint8_t id[SBMP_COMM_ID_BYTES], int nranks,
+                                     int rank, sbmp_kgmt** out) {
+    return guarded([&] {
+        REQUIRE(p && id && out, "NULL argument");
+        REQUIRE(nranks >= 1 && rank >= 0 && rank < nranks, "bad rank/nranks");
+        *out = nullptr;
+        sbmp_kgmt* h = new sbmp_kgmt;
+        try {
+            if (nranks > 1) {
+                h->comm = sbmp::sharded_create_comm(id, nranks, rank, p->device);
+                h->planner = new KgmtPlanner(*p, nranks, rank, sbmp::sharded_exchange(h->comm));
+            } else {
+                h->planner = new KgmtPlanner(*p);
+            }
+        } catch (...) {
+            delete h->planner;
+            if (h->comm) sbmp::sharded_destroy_comm(h->comm);
+            delete h;
+            throw;
+        }
+        *out = h;
+    });
+}
+
+sbmp_status sbmp_comm_get_unique_id(uint8_t id[SBMP_COMM_ID_BYTES]) {
+    return guarded([&] {
+        REQUIRE(id, "NULL id");
+        sbmp::comm_get_unique_id(id);
+    });
+}
+
+sbmp_status sbmp_kgmt_destroy(sbmp_kgmt* h) {
+    return guarded([&] {
+        if (!h) return;
+        delete h->planner;
+        if (h->comm) sbmp::sharded_destroy_comm(h->comm);
+        delete h;
+    });
+}
+
+#define PLANNER(h)                                                     \
+    REQUIRE((h) && (h)->planner, "NULL planner handle");               \
+    KgmtPlanner& P = *(h)->planner
+
+sbmp_status sbmp_kgmt_begin(sbmp_kgmt* h, const float initial[7], const float goal[7], const float* d_obstacles,
+                            int obstaclesCount, uint64_t seed) {
+    return guarded([&] {
+        PLANNER(h);
+        P.begin(initial, goal, d_obstacles, obstaclesCount, seed);
+    });
+}
+
+sbmp_status sbmp_kgmt_plan(sbmp_kgmt* h, const float initial[7], const float goal[7], const float* d_obstacles,
+                           int obstaclesCount, uint64_t seed, sbmp_plan_result* result) {
+    return guarded([&] {
+        PLANNER(h);
+        P.begin(initial, goal, d_obstacles, obstaclesCount, seed);
+        // Poll every 8 iterations: the kernels of a finished loop are no-ops, so
+        // over-enqueueing costs a few microseconds, not correctness.
+        P.run(8);
+        if (result) P.result(result);
+    });
+}
+
+sbmp_status sbmp_kgmt_step(sbmp_kgmt* h, int iterations, int* active) {
+    return guarded([&] {
+        PLANNER(h);
+        REQUIRE(iterations >= 0, "iterations must be >= 0");
+        P.enqueue(iterations);
+        const bool a = P.active();
+        if (active) *active = a ? 1 : 0;
+    });
+}
+
+sbmp_status sbmp_kgmt_enqueue(sbmp_kgmt* h, int iterations) {
+    return guarded([&] {
+        PLANNER(h);
+        REQUIRE(iterations >= 0, "iterations must be >= 0");
+        P.enqueue(iterations);
+    });
+}
+
+sbmp_status sbmp_kgmt_sync(sbmp_kgmt* h) {
+    return guarded([&] {
+        PLANNER(h);
+        P.sync();
+    });
+}
+
+sbmp_status sbmp_kgmt_result(sbmp_kgmt* h, sbmp_plan_result* result) {
+    return guarded([&] {
+        PLANNER(h);
+        REQUIRE(result, "NULL result");
+        P.result(result);
+    });
+}
+
+sbmp_status sbmp_kgmt_stream(sbmp_kgmt* h, void** stream) {
+    return guarded([&] {
+        PLANNER(h);
+        REQUIRE(stream, "NULL stream");
+        *stream = (void*)P.stream();
+    });
+}
+
+sbmp_status sbmp_kgmt_copy_tree(sbmp_kgmt* h, float* samples, int* parent, float* costs, int capacity) {
+    return guarded([&] {
+        PLANNER(h);
+        REQUIRE(capacity >= P.params().maxTreeSize, "capacity < maxTreeSize");
+        P.copy_tree(samples, parent, costs);
+    });
+}
+
+sbmp_status sbmp_kgmt_copy_unexplored(sbmp_kgmt* h, float* samples, int* uParent, int capacity) {
+    return guarded([&] {
+        PLANNER(h);
+        REQUIRE(capacity >= P.params().maxTreeSize, "capacity < maxTreeSize");
+        P.copy_unexplored(samples, uParent);
+    });
+}
+
+sbmp_status sbmp_kgmt_copy_flags(sbmp_kgmt* h, uint8_t* G, uint8_t* GNew, int capacity) {
+    return guarded([&] {
+        PLANNER(h);
+        REQUIRE(capacity >= P.params().maxTreeSize, "capacity < maxTreeSize");
+        P.copy_flags(G, GNew);
+    });
+}
+
+sbmp_status sbmp_kgmt_copy_regions(sbmp_kgmt* h, int* R1, int* R1Avail, int* R1Valid, int* R1Invalid, float* R1Score,
+                                   int* R2Avail, int* R2Valid, int* R2Invalid) {
+    return guarded([&] {
+        PLANNER(h);
+        P.copy_regions(R1, R1Avail, R1Valid, R1Invalid, R1Score, R2Avail, R2Valid, R2Invalid);
+    });
+}
+
+sbmp_status sbmp_kgmt_num_slots(sbmp_kgmt* h, int* slots) {
+    return guarded([&] {
+        PLANNER(h);
+        REQUIRE(slots, "NULL slots");
+        *slots = P.num_slots();
+    });
+}
+
+sbmp_status sbmp_kgmt_copy_rng(sbmp_kgmt* h, uint32_t* states, int capacity) {
+    return guarded([&] {
+        PLANNER(h);
+        REQUIRE(states && capacity >= P.num_slots(), "capacity < num_slots");
+        P.copy_rng(states);
+    });
+}
+
+sbmp_status sbmp_kgmt_iter_log(sbmp_kgmt* h, sbmp_iter_record* out, int capacity, int* count) {
+    return guarded([&] {
+        PLANNER(h);
+        std::vector<sbmp_iter_record> log = P.iter_log();
+        const int n = std::min<int>(capacity, (int)log.size());
+        if (out && n > 0) memcpy(out, log.data(), sizeof(sbmp_iter_record) * n);
+        if (count) *count = (int)log.size();
+    });
+}
+
+sbmp_status sbmp_kgmt_export_csv(sbmp_kgmt* h, const char* dir) {
+    return guarded([&] {
+        PLANNER(h);
+        P.export_csv(dir ? dir : "");
+    });
+}
+
+sbmp_status sbmp_kgmt_kernel_stats(sbmp_kgmt* h, sbmp_kernel_stat* out, int capacity, int* count) {
+    return guarded([&] {
+        PLANNER(h);
+        std::vector<sbmp_kernel_stat> st = P.kernel_stats();
+        const int n = std::min<int>(capacity, (int)st.size());
+        if (out && n > 0) memcpy(out, st.data(), sizeof(sbmp_kernel_stat) * n);
+        if (count) *count = (int)st.size();
+    });
+}
+
+sbmp_status sbmp_kgmt_reset_kernel_stats(sbmp_kgmt* h) {
+    return guarded([&] {
+        PLANNER(h);
+        P.reset_kernel_stats();
+    });
+}
+
+// readObstaclesFromCSV (reference src/helper/helper.cu:11-34): values separated
+// by whitespace or single commas, read line by line with operator>>.
+sbmp_status sbmp_read_obstacles_csv(const char* path, int workspaceDim, float* out, int capacity,
+                                    int* numObstacles) {
+    return guarded([&] {
+        REQUIRE(path && numObstacles && workspaceDim > 0, "bad argument");
+        std::ifstream file(path);
+        if (!file.is_open()) throw Error(SBMP_ERR_IO, std::string("Error opening file: ") + path);
+        std::vector<float> v;
+        std::string line;
+        while (std::getline(file, line)) {
+            std::stringstream ss(line);
+            float value;
+            while (ss >> value) {
+                v.push_back(value);
+                if (ss.peek() == ',') ss.ignore();
+            }
+        }
+        const int n = (int)(v.size() / (2 * workspaceDim));
+        *numObstacles = n;
+        if (out) {
+            REQUIRE(capacity >= (int)v.size(), "capacity smaller than the file's float count");
+            memcpy(out, v.data(), sizeof(float) * v.size());
+        }
+    });
+}
+
+sbmp_status sbmp_device_upload_f32(const float* host, size_t count, float** d_out) {
+    return guarded([&] {
+        REQUIRE(d_out && (host || count == 0), "bad argument");
+        void* p = nullptr;
+        SBMP_HIP(hipMalloc(&p, std::max<size_t>(count, 1) * sizeof(float)));
+        if (count) {
+            hipError_t e = hipMemcpy(p, host, count * sizeof(float), hipMemcpyHostToDevice);
+            if (e != hipSuccess) {
+                hipFree(p);
+                SBMP_HIP(e);
+            }
+        }
+        *d_out = static_cast<float*>(p);
+    });
+}
+
+sbmp_status sbmp_device_free(void* d_ptr) {
+    return guarded([&] {
+        if (d_ptr) SBMP_HIP(hipFree(d_ptr));
+    });
+}
+
+sbmp_status sbmp_device_count(int* count) {
+    return guarded([&] {
+        REQUIRE(count, "NULL count");
+        int n = 0;
+        hipError_t e = hipGetDeviceCount(&n);
+        *count = (e == hipSuccess) ? n : 0;
+    });
+}
+
+}  // extern "C"

@@ -1,0 +1,265 @@
+"""Python mirror of the reference planner interface, backed by libsbmp.so.
+
+Reference: class KGMT (include/planners/KGMT.cuh:23-109)
+    KGMT(float width, float height, int N, int n, int numIterations, int maxTreeSize,
+         int numDisc, float agentLength, float goalThreshold)
+    void plan(float* initial, float* goal, float* d_obstacles, int obstaclesCount)
+    public fields treeSize_, costToGoal_, numIterations_, maxTreeSize_, numDisc_, width_,
+                  height_, agentLength_, goalThreshold_, N_, n_, R1Size_, R2Size_
+The reference seeds curand with time(NULL) inside plan() (KGMT.cu:111); here the
+seed is an optional keyword (default: time(NULL) converted int -> unsigned long
+long exactly as the reference's initCurandStates(..., int seed) call does).
+"""
+from __future__ import annotations
+
+import ctypes
+import time
+from typing import Optional
+
+import numpy as np
+
+from . import _native as nat
+
+AGENTS = {"car": nat.SBMP_AGENT_CAR, "point": nat.SBMP_AGENT_POINT}
+
+
+def reference_seed_from_time(t: Optional[float] = None) -> int:
+    """time(NULL) -> int -> unsigned long long (sign-extended), as KGMT.cu:111 + curand_init."""
+    v = ctypes.c_int(int(time.time() if t is None else t)).value
+    return v & 0xFFFFFFFFFFFFFFFF
+
+
+class DeviceBuffer:
+    """A float32 device array allocated through the ABI (demos/main.cu:60-61 cudaMalloc+cudaMemcpy)."""
+
+    def __init__(self, host: np.ndarray):
+        host = np.ascontiguousarray(host, dtype=np.float32).ravel()
+        p = ctypes.c_void_p()
+        nat.call("sbmp_device_upload_f32", host.ctypes.data_as(ctypes.c_void_p), host.size, ctypes.byref(p))
+        self.ptr = p.value or 0
+        self.count = host.size
+
+    def free(self):
+        if self.ptr:
+            nat.call("sbmp_device_free", ctypes.c_void_p(self.ptr))
+            self.ptr = 0
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+def device_ptr(obj) -> int:
+    """Device address of a DeviceBuffer, a torch tensor on the GPU, or a raw int."""
+    if obj is None:
+        return 0
+    if isinstance(obj, DeviceBuffer):
+        return obj.ptr
+    if isinstance(obj, int):
+        return obj
+    if hasattr(obj, "data_ptr"):
+        if hasattr(obj, "is_cuda") and not obj.is_cuda:
+            raise ValueError("d_obstacles must live in device memory")
+        return obj.data_ptr()
+    raise TypeError(f"cannot take a device pointer of {type(obj)!r}")
+
+
+def read_obstacles_csv(path: str, workspace_dim: int = 2) -> np.ndarray:
+    """readObstaclesFromCSV (reference src/helper/helper.cu:11-34) through the ABI; (count, 4) float32."""
+    n = ctypes.c_int()
+    nat.call("sbmp_read_obstacles_csv", path.encode(), workspace_dim, None, 0, ctypes.byref(n))
+    cap = max(1, n.value * 2 * workspace_dim + 2 * workspace_dim)
+    buf = np.zeros(cap, dtype=np.float32)
+    nat.call("sbmp_read_obstacles_csv", path.encode(), workspace_dim, buf.ctypes.data_as(ctypes.c_void_p), cap,
+             ctypes.byref(n))
+    return buf[: n.value * 2 * workspace_dim].reshape(n.value, 2 * workspace_dim).copy()
+
+
+def device_count() -> int:
+    n = ctypes.c_int()
+    nat.call("sbmp_device_count", ctypes.byref(n))
+    return n.value
+
+
+def _vec7(v) -> np.ndarray:
+    a = np.zeros(7, dtype=np.float32)
+    v = np.asarray(v, dtype=np.float32).ravel()
+    a[: len(v)] = v
+    return a
+
+
+class KGMT:
+    """MI355X KGMT planner with the reference's constructor and plan() signature."""
+
+    def __init__(self, width: float, height: float, N: int, n: int, numIterations: int, maxTreeSize: int,
+                 numDisc: int, agentLength: float, goalThreshold: float, *, samplesPerIteration: int = 0,
+                 agent: str = "car", fixGNewClear: bool = False, device: int = 0, profileKernels: bool = False,
+                 _sharded=None):
+        p = nat.KgmtParams()
+        nat.call("sbmp_kgmt_default_params", ctypes.byref(p))
+        p.width, p.height, p.N, p.n = width, height, N, n
+        p.numIterations, p.maxTreeSize, p.numDisc = numIterations, maxTreeSize, numDisc
+        p.agentLength, p.goalThreshold = agentLength, goalThreshold
+        p.samplesPerIteration = samplesPerIteration
+        p.agent = AGENTS[agent]
+        p.fixGNewClear = int(bool(fixGNewClear))
+        p.device = device
+        p.profileKernels = int(bool(profileKernels))
+        self._params = p
+        h = ctypes.c_void_p()
+        if _sharded is None:
+            nat.call("sbmp_kgmt_create", ctypes.byref(p), ctypes.byref(h))
+        else:
+            uid, nranks, rank = _sharded
+            idbuf = (ctypes.c_uint8 * nat.SBMP_COMM_ID_BYTES).from_buffer_copy(bytes(uid))
+            nat.call("sbmp_kgmt_create_sharded", ctypes.byref(p), idbuf, nranks, rank, ctypes.byref(h))
+        self._h = h
+        # reference public fields (KGMT.cuh:34-43, 103-106)
+        self.width_, self.height_, self.N_, self.n_ = float(width), float(height), N, n
+        self.numIterations_, self.maxTreeSize_, self.numDisc_ = numIterations, maxTreeSize, numDisc
+        self.agentLength_, self.goalThreshold_ = float(agentLength), float(goalThreshold)
+        self.R1Size_ = float(np.float32(width) / np.float32(N))
+        self.R2Size_ = float(np.float32(width) / np.float32(n * N))
+        self.treeSize_ = 0
+        self.costToGoal_ = 0.0
+        self.last_result: Optional[nat.PlanResult] = None
+        self._obs_keepalive = None
+
+    @classmethod
+    def from_params(cls, **kw) -> "KGMT":
+        base = dict(width=20.0, height=20.0, N=16, n=8, numIterations=100, maxTreeSize=30000, numDisc=10,
+                    agentLength=1.0, goalThreshold=0.5)
+        base.update(kw)
+        return cls(**base)
+
+    def close(self):
+        if getattr(self, "_h", None) and self._h.value:
+            nat.call("sbmp_kgmt_destroy", self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def M(self) -> int:
+        return self.maxTreeSize_
+
+    # ---------------------------------------------------------------- planning
+    def plan(self, initial, goal, d_obstacles, obstaclesCount: int, seed: Optional[int] = None) -> nat.PlanResult:
+        """KGMT::plan (reference KGMT.cu:80-317); blocking."""
+        seed = reference_seed_from_time() if seed is None else seed
+        i, g = _vec7(initial), _vec7(goal)
+        r = nat.PlanResult()
+        self._obs_keepalive = d_obstacles
+        nat.call("sbmp_kgmt_plan", self._h, i.ctypes.data_as(ctypes.c_void_p), g.ctypes.data_as(ctypes.c_void_p),
+                 ctypes.c_void_p(device_ptr(d_obstacles)), obstaclesCount, seed, ctypes.byref(r))
+        self._absorb(r)
+        return r
+
+    def begin(self, initial, goal, d_obstacles, obstaclesCount: int, seed: int) -> None:
+        i, g = _vec7(initial), _vec7(goal)
+        self._obs_keepalive = d_obstacles
+        nat.call("sbmp_kgmt_begin", self._h, i.ctypes.data_as(ctypes.c_void_p), g.ctypes.data_as(ctypes.c_void_p),
+                 ctypes.c_void_p(device_ptr(d_obstacles)), obstaclesCount, seed)
+
+    def step(self, iterations: int = 1) -> bool:
+        """Run up to `iterations` more loop iterations; False once the loop has ended."""
+        a = ctypes.c_int()
+        nat.call("sbmp_kgmt_step", self._h, iterations, ctypes.byref(a))
+        return bool(a.value)
+
+    def enqueue(self, iterations: int) -> None:
+        nat.call("sbmp_kgmt_enqueue", self._h, iterations)
+
+    def sync(self) -> None:
+        nat.call("sbmp_kgmt_sync", self._h)
+
+    def result(self) -> nat.PlanResult:
+        r = nat.PlanResult()
+        nat.call("sbmp_kgmt_result", self._h, ctypes.byref(r))
+        self._absorb(r)
+        return r
+
+    def _absorb(self, r: nat.PlanResult) -> None:
+        self.treeSize_ = r.treeSize
+        self.costToGoal_ = r.costToGoal
+        self.last_result = r
+
+    def stream(self) -> int:
+        s = ctypes.c_void_p()
+        nat.call("sbmp_kgmt_stream", self._h, ctypes.byref(s))
+        return s.value or 0
+
+    # ---------------------------------------------------------------- state export
+    def tree(self):
+        M = self.M
+        s = np.zeros((M, 7), dtype=np.float32)
+        p = np.zeros(M, dtype=np.int32)
+        c = np.zeros(M, dtype=np.float32)
+        nat.call("sbmp_kgmt_copy_tree", self._h, s.ctypes.data_as(ctypes.c_void_p),
+                 p.ctypes.data_as(ctypes.c_void_p), c.ctypes.data_as(ctypes.c_void_p), M)
+        return s, p, c
+
+    def unexplored(self):
+        M = self.M
+        s = np.zeros((M, 7), dtype=np.float32)
+        p = np.zeros(M, dtype=np.int32)
+        nat.call("sbmp_kgmt_copy_unexplored", self._h, s.ctypes.data_as(ctypes.c_void_p),
+                 p.ctypes.data_as(ctypes.c_void_p), M)
+        return s, p
+
+    def flags(self):
+        M = self.M
+        g = np.zeros(M, dtype=np.uint8)
+        gn = np.zeros(M, dtype=np.uint8)
+        nat.call("sbmp_kgmt_copy_flags", self._h, g.ctypes.data_as(ctypes.c_void_p),
+                 gn.ctypes.data_as(ctypes.c_void_p), M)
+        return g, gn
+
+    def regions(self) -> dict:
+        n1 = self.N_ * self.N_
+        n2 = n1 * self.n_ * self.n_
+        r = {k: np.zeros(n1, dtype=np.int32) for k in ("R1", "R1Avail", "R1Valid", "R1Invalid")}
+        r["R1Score"] = np.zeros(n1, dtype=np.float32)
+        for k in ("R2Avail", "R2Valid", "R2Invalid"):
+            r[k] = np.zeros(n2, dtype=np.int32)
+        order = ("R1", "R1Avail", "R1Valid", "R1Invalid", "R1Score", "R2Avail", "R2Valid", "R2Invalid")
+        nat.call("sbmp_kgmt_copy_regions", self._h, *[r[k].ctypes.data_as(ctypes.c_void_p) for k in order])
+        return r
+
+    def num_slots(self) -> int:
+        n = ctypes.c_int()
+        nat.call("sbmp_kgmt_num_slots", self._h, ctypes.byref(n))
+        return n.value
+
+    def rng(self) -> np.ndarray:
+        n = self.num_slots()
+        out = np.zeros((n, 6), dtype=np.uint32)
+        nat.call("sbmp_kgmt_copy_rng", self._h, out.ctypes.data_as(ctypes.c_void_p), n)
+        return out
+
+    def iter_log(self) -> np.ndarray:
+        cnt = ctypes.c_int()
+        nat.call("sbmp_kgmt_iter_log", self._h, None, 0, ctypes.byref(cnt))
+        arr = (nat.IterRecord * max(1, cnt.value))()
+        nat.call("sbmp_kgmt_iter_log", self._h, ctypes.cast(arr, ctypes.c_void_p), cnt.value, ctypes.byref(cnt))
+        return np.array([[getattr(arr[i], k) for k in nat.ITER_FIELDS] for i in range(cnt.value)],
+                        dtype=np.int64).reshape(-1, len(nat.ITER_FIELDS))
+
+    def export_csv(self, directory: str) -> None:
+        """The 13 CSV dumps of KGMT.cu:299-311."""
+        nat.call("sbmp_kgmt_export_csv", self._h, directory.encode())
+
+    def kernel_stats(self) -> dict:
+        cnt = ctypes.c_int()
+        arr = (nat.KernelStat * 16)()
+        nat.call("sbmp_kgmt_kernel_stats", self._h, ctypes.cast(arr, ctypes.c_void_p), 16, ctypes.byref(cnt))
+        return {arr[i].name.decode(): (arr[i].launches, arr[i].totalMs) for i in range(min(cnt.value, 16))}
+
+    def reset_kernel_stats(self) -> None:
+        nat.call("sbmp_kgmt_reset_kernel_stats", self._h)

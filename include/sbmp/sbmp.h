@@ -1,0 +1,168 @@
+/* sbmp.h — C ABI of the MI355X-native KGMT planner (libsbmp.so).
+ *
+ * The reference (nipe1783/cudaSBMP) exposes one planner, the C++ class KGMT
+ * (reference include/planners/KGMT.cuh:23-109), driven by demos/main.cu.  This
+ * ABI is the thin, plain-pointer boundary that replaces it; the C++ facade in
+ * include/planners/KGMT.h rebuilds the reference's class on top of it, so
+ * demos/main.cpp stays a drop-in for demos/main.cu.
+ *
+ * Conventions
+ *   - Every call returns sbmp_status (0 = SBMP_OK).  On failure
+ *     sbmp_last_error() describes the cause.  (The reference has no error
+ *     codes: CUDA_ERROR_CHECK prints and exit(1)s, include/helper/helper.cuh:19-27,
+ *     and the KGMT kernel launches are unchecked.)
+ *   - Host arrays are plain C arrays; device arrays are HIP device pointers
+ *     (d_ prefix), exactly as the reference's plan() takes d_obstacles.
+ *   - One planner handle = one HIP stream on one device; a handle is not
+ *     thread-safe.  plan()/begin() may be called repeatedly on one handle
+ *     (the reference's plan() is single-shot: it frees ctor-owned buffers,
+ *     KGMT.cu:314-316).
+ */
+#ifndef SBMP_H
+#define SBMP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SBMP_ABI_VERSION 1
+
+typedef int sbmp_status;
+#define SBMP_OK 0
+#define SBMP_ERR_INVALID_ARGUMENT 1
+#define SBMP_ERR_HIP 2
+#define SBMP_ERR_IO 3
+#define SBMP_ERR_OUT_OF_MEMORY 4
+#define SBMP_ERR_STATE 5
+#define SBMP_ERR_UNSUPPORTED 6
+#define SBMP_ERR_COMM 7
+
+#define SBMP_AGENT_CAR 0   /* kinematic bicycle, reference src/statePropagator/statePropagator.cu:5-76 */
+#define SBMP_AGENT_POINT 1 /* holonomic R2 point (build extension, no reference counterpart) */
+
+#define SBMP_SAMPLE_DIM 7  /* [x, y, theta, v, a, steering, duration], reference KGMT.cu:5, State.h:6-20 */
+
+/* Constructor arguments of KGMT::KGMT (reference KGMT.cuh:28, KGMT.cu:10-78)
+ * plus the build's knobs. */
+typedef struct sbmp_kgmt_params {
+    float width, height;      /* workspace extent */
+    int N, n;                 /* R1 grid N x N (N must be 16, KGMT.cu:8); R2 sub-grid n x n per R1 cell (1..16) */
+    int numIterations;        /* loop bound, KGMT.cu:118 */
+    int maxTreeSize;          /* tree capacity M */
+    int numDisc;              /* Euler sub-steps per child, statePropagator.cu:33 */
+    float agentLength;        /* bicycle wheelbase, statePropagator.cu:58 */
+    float goalThreshold;      /* goal radius, KGMT.cu:635-638 (0 disables the goal) */
+    int samplesPerIteration;  /* 0 = reference batch rule (KGMT.cu:151-219); S > 0 = capped extension */
+    int agent;                /* SBMP_AGENT_* */
+    int fixGNewClear;         /* 0 = reproduce the reference's partial GNew clear */
+    int device;               /* HIP device ordinal */
+    int profileKernels;       /* 1 = time every kernel launch with HIP events (sbmp_kgmt_kernel_stats) */
+} sbmp_kgmt_params;
+
+/* Outcome of a plan (the reference's public fields treeSize_/costToGoal_, KGMT.cuh:37,40,
+ * plus what its prints report, KGMT.cu:295-296). */
+typedef struct sbmp_plan_result {
+    int iterations;           /* loop iterations executed */
+    int treeSize;             /* treeSize_ (may exceed maxTreeSize on the final iteration, as in the reference) */
+    float costToGoal;         /* costToGoal_: cost of the first goal node, 0 if none */
+    int goalIndex;            /* tree row of that node, -1 if none (D4: lowest row of the first goal iteration) */
+    long long samplesGenerated; /* children propagated and collision-checked, all iterations */
+    long long accepted;       /* nodes appended to the tree, all iterations */
+    double wallMs;            /* device-synchronised wall time of the iteration loop */
+    int stalled;              /* 1 if the loop ended with an empty frontier (D7) */
+} sbmp_plan_result;
+
+/* Per-iteration bookkeeping (same fields as the oracle's log). */
+typedef struct sbmp_iter_record {
+    int itr, treeSizeBefore, nG, k, nExp, S, A, treeSizeAfter, goalIdx;
+} sbmp_iter_record;
+
+typedef struct sbmp_kernel_stat {
+    char name[32];
+    long long launches;
+    double totalMs;           /* sum of HIP-event durations on the planner's stream */
+} sbmp_kernel_stat;
+
+typedef struct sbmp_kgmt sbmp_kgmt;
+
+int sbmp_abi_version(void);
+const char* sbmp_status_string(sbmp_status s);
+const char* sbmp_last_error(void);
+
+/* The demo configuration, reference demos/main.cu:19-28. */
+sbmp_status sbmp_kgmt_default_params(sbmp_kgmt_params* p);
+
+/* KGMT::KGMT (KGMT.cu:10-78): allocates every planner buffer on p->device. */
+sbmp_status sbmp_kgmt_create(const sbmp_kgmt_params* p, sbmp_kgmt** out);
+sbmp_status sbmp_kgmt_destroy(sbmp_kgmt* h);
+
+/* KGMT::plan (KGMT.cu:80-317): root init, RNG init (curand_init(seed, slot, 0),
+ * KGMT.cu:111 — the reference seeds with time(NULL); here the seed is explicit),
+ * iterate until goal / full tree / numIterations.  initial and goal are host
+ * arrays of 7 floats; d_obstacles is a device array of obstaclesCount boxes
+ * [xmin, ymin, xmax, ymax] (reference collisionCheck.cu:7-14).  Blocking. */
+sbmp_status sbmp_kgmt_plan(sbmp_kgmt* h, const float initial[7], const float goal[7], const float* d_obstacles,
+                           int obstaclesCount, uint64_t seed, sbmp_plan_result* result);
+
+/* Stepwise form of plan: begin = prologue (KGMT.cu:84-116); step enqueues up to
+ * `iterations` more loop iterations and waits for them (*active = 0 once the
+ * loop has ended); result reads the outcome. */
+sbmp_status sbmp_kgmt_begin(sbmp_kgmt* h, const float initial[7], const float goal[7], const float* d_obstacles,
+                            int obstaclesCount, uint64_t seed);
+sbmp_status sbmp_kgmt_step(sbmp_kgmt* h, int iterations, int* active);
+/* Enqueue iterations without waiting (device-resident loop; kernels become
+ * no-ops once the loop has ended).  sbmp_kgmt_sync waits for the stream. */
+sbmp_status sbmp_kgmt_enqueue(sbmp_kgmt* h, int iterations);
+sbmp_status sbmp_kgmt_sync(sbmp_kgmt* h);
+sbmp_status sbmp_kgmt_result(sbmp_kgmt* h, sbmp_plan_result* result);
+/* The HIP stream (hipStream_t) every kernel of this planner runs on. */
+sbmp_status sbmp_kgmt_stream(sbmp_kgmt* h, void** stream);
+
+/* State export in the reference's layouts (thrust vectors of KGMT.cuh:44-68):
+ * samples M x 7 AoS, parents M, costs M, bools as bytes.  capacity = rows of
+ * the caller's arrays (must be >= maxTreeSize).  Any pointer may be NULL. */
+sbmp_status sbmp_kgmt_copy_tree(sbmp_kgmt* h, float* samples, int* parent, float* costs, int capacity);
+sbmp_status sbmp_kgmt_copy_unexplored(sbmp_kgmt* h, float* samples, int* uParent, int capacity);
+sbmp_status sbmp_kgmt_copy_flags(sbmp_kgmt* h, uint8_t* G, uint8_t* GNew, int capacity);
+/* R1* arrays have N*N entries, R2* arrays N*N*n*n. */
+sbmp_status sbmp_kgmt_copy_regions(sbmp_kgmt* h, int* R1, int* R1Avail, int* R1Valid, int* R1Invalid, float* R1Score,
+                                   int* R2Avail, int* R2Valid, int* R2Invalid);
+/* XORWOW state per slot: 6 words {v0..v4, d}.  Slots = sbmp_kgmt_num_slots. */
+sbmp_status sbmp_kgmt_num_slots(sbmp_kgmt* h, int* slots);
+sbmp_status sbmp_kgmt_copy_rng(sbmp_kgmt* h, uint32_t* states, int capacity);
+sbmp_status sbmp_kgmt_iter_log(sbmp_kgmt* h, sbmp_iter_record* out, int capacity, int* count);
+/* The 13 CSV dumps of KGMT.cu:299-311 (std::fixed, 10 decimals, helper.cuh:53-72) into dir. */
+sbmp_status sbmp_kgmt_export_csv(sbmp_kgmt* h, const char* dir);
+
+sbmp_status sbmp_kgmt_kernel_stats(sbmp_kgmt* h, sbmp_kernel_stat* out, int capacity, int* count);
+sbmp_status sbmp_kgmt_reset_kernel_stats(sbmp_kgmt* h);
+
+/* readObstaclesFromCSV (reference src/helper/helper.cu:11-34): whitespace or
+ * comma separated floats, numObstacles = floats / (2*workspaceDim).  Returns
+ * SBMP_ERR_IO instead of exit(1) when the file cannot be opened.  With
+ * out == NULL only *numObstacles is computed. */
+sbmp_status sbmp_read_obstacles_csv(const char* path, int workspaceDim, float* out, int capacity, int* numObstacles);
+
+/* Device memory helpers replacing demos/main.cu:60-61,64 (cudaMalloc/cudaMemcpy/cudaFree). */
+sbmp_status sbmp_device_upload_f32(const float* host, size_t count, float** d_out);
+sbmp_status sbmp_device_free(void* d_ptr);
+sbmp_status sbmp_device_count(int* count);
+
+/* ---- Multi-GPU: one planning problem sharded over ranks (one process per GPU) ----
+ * Slots are owned block-cyclically (slot s -> rank (s/256) mod nranks); every
+ * rank keeps a full replica of the tree; per iteration the ranks all-reduce
+ * the region-counter deltas and all-gather the accepted children over RCCL,
+ * so every rank builds the same tree as a 1-GPU run with the same seed. */
+#define SBMP_COMM_ID_BYTES 128
+sbmp_status sbmp_comm_get_unique_id(uint8_t id[SBMP_COMM_ID_BYTES]);
+sbmp_status sbmp_kgmt_create_sharded(const sbmp_kgmt_params* p, const uint8_t id[SBMP_COMM_ID_BYTES], int nranks,
+                                     int rank, sbmp_kgmt** out);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* SBMP_H */

@@ -647,6 +647,55 @@ void oracle_xorwow_draw(uint32_t state[6], int count, uint32_t* out) {
     state[5] = st.d;
 }
 
+// Replay (invariant I1; the reference's MATLAB replay, visualizationKGMT_Single.m:79-116):
+// re-propagate parent state p[i][0..3] with the stored controls u[i] = (a, steering, duration)
+// for numDisc steps; out[i] = (x, y, theta, v), valid[i] = motion validity.
+void oracle_replay(const oracle_params* prm, const float* obstacles, int nObs, const float* parents,
+                   const float* controls, int n, float* out, uint8_t* valid) {
+    PropCfg pc{prm->numDisc, prm->agentLength, prm->width, prm->height, obstacles, nObs};
+#pragma omp parallel for schedule(static) num_threads(prm->threads > 0 ? prm->threads : 1)
+    for (int i = 0; i < n; ++i) {
+        const float* p = &parents[4 * i];
+        const float* u = &controls[3 * i];
+        const float dt = u[2] / (float)pc.numDisc;
+        float x = p[0], y = p[1], theta = p[2], v = p[3];
+        bool ok = true;
+        const float tan_steering = prm->agent == 1 ? 0.0f : sbmp::tanf_d(u[1]);
+        for (int k = 0; k < pc.numDisc; ++k) {
+            const float v_state[WS_DIM] = {x, y};
+            if (prm->agent == 1) {
+                x = fmaf(u[0], dt, x);
+                y = fmaf(u[1], dt, y);
+            } else {
+                float st, ct;
+                sbmp::sincosf_d(theta, &st, &ct);
+                x = fmaf(v * ct, dt, x);
+                y = fmaf(v * st, dt, y);
+            }
+            if (x <= 0.0f || x >= pc.width || y <= 0.0f || y >= pc.height) {
+                ok = false;
+                break;
+            }
+            if (prm->agent != 1) {
+                theta = fmaf((v / pc.agentLength) * tan_steering, dt, theta);
+                v = fmaf(u[0], dt, v);
+            }
+            const float w_state[WS_DIM] = {x, y};
+            float bbMin[WS_DIM], bbMax[WS_DIM];
+            segment_aabb(v_state, w_state, bbMin, bbMax);
+            if (!isMotionValid(bbMin, bbMax, pc.obstacles, pc.obstaclesCount)) {
+                ok = false;
+                break;
+            }
+        }
+        out[4 * i] = x;
+        out[4 * i + 1] = y;
+        out[4 * i + 2] = prm->agent == 1 ? 0.0f : theta;
+        out[4 * i + 3] = prm->agent == 1 ? 0.0f : v;
+        valid[i] = ok ? 1 : 0;
+    }
+}
+
 void oracle_sincosf(const float* x, int n, float* s, float* c) {
     for (int i = 0; i < n; ++i) sbmp::sincosf_d(x[i], &s[i], &c[i]);
 }

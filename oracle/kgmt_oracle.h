@@ -86,6 +86,11 @@ long long oracle_samples_generated(void* h);
 void oracle_xorwow_init(uint64_t seed, uint64_t subsequence, int seeding, uint32_t state[6]);
 void oracle_xorwow_draw(uint32_t state[6], int count, uint32_t* out);
 
+/* Invariant I1: re-propagate parents (n x 4) with stored controls (n x 3: a, steering,
+ * duration) -> out (n x 4), valid (n).  Uses prm's agent, numDisc, agentLength, workspace. */
+void oracle_replay(const oracle_params* prm, const float* obstacles, int nObs, const float* parents,
+                   const float* controls, int n, float* out, uint8_t* valid);
+
 /* Deterministic math exposed for tests. */
 void oracle_sincosf(const float* x, int n, float* s, float* c);
 void oracle_tanf(const float* x, int n, float* t);

@@ -86,6 +86,7 @@ def lib():
         L.oracle_samples_generated.restype = ctypes.c_longlong
         L.oracle_xorwow_init.argtypes = [u64, u64, i, vp]
         L.oracle_xorwow_draw.argtypes = [vp, i, vp]
+        L.oracle_replay.argtypes = [P(OracleParams), vp, i, vp, vp, i, vp, vp]
         L.oracle_sincosf.argtypes = [vp, i, vp, vp]
         L.oracle_tanf.argtypes = [vp, i, vp]
         _lib = L
@@ -227,6 +228,22 @@ class Oracle:
         n = lib().oracle_iter_logs(self._h, ctypes.cast(arr, ctypes.c_void_p), cap)
         names = [f[0] for f in OracleIterLog._fields_]
         return np.array([[getattr(arr[i], k) for k in names] for i in range(n)], dtype=np.int64).reshape(-1, len(names))
+
+
+def replay(cfg: PlannerConfig, obstacles, parents: np.ndarray, controls: np.ndarray, threads: int = 8):
+    """Invariant I1: re-propagate parents (n,4) with controls (n,3) -> (states (n,4), valid (n,))."""
+    p = OracleParams(cfg.width, cfg.height, cfg.N, cfg.n, cfg.numIterations, cfg.maxTreeSize, cfg.numDisc,
+                     cfg.agentLength, cfg.goalThreshold, cfg.samplesPerIteration, cfg.agent, cfg.fixGNewClear,
+                     threads, 1, 0)
+    obs = np.ascontiguousarray(obstacles, dtype=np.float32).ravel()
+    parents = np.ascontiguousarray(parents, dtype=np.float32)
+    controls = np.ascontiguousarray(controls, dtype=np.float32)
+    n = len(parents)
+    out = np.zeros((n, 4), dtype=np.float32)
+    valid = np.zeros(n, dtype=np.uint8)
+    lib().oracle_replay(ctypes.byref(p), _fp(obs), len(obs) // 4, _fp(parents), _fp(controls), n, _fp(out),
+                        _fp(valid))
+    return out, valid.astype(bool)
 
 
 def xorwow_init(seed: int, subsequence: int, seeding: str = "curand") -> np.ndarray:
