@@ -15,6 +15,8 @@ SBMP_OK = 0
 SBMP_AGENT_CAR = 0
 SBMP_AGENT_POINT = 1
 SBMP_COMM_ID_BYTES = 128
+SBMP_BATCH_REFERENCE = 0
+SBMP_BATCH_FILL = 1
 
 
 class NativeLibraryError(RuntimeError):
@@ -34,7 +36,7 @@ class KgmtParams(ctypes.Structure):
         ("numIterations", ctypes.c_int), ("maxTreeSize", ctypes.c_int), ("numDisc", ctypes.c_int),
         ("agentLength", ctypes.c_float), ("goalThreshold", ctypes.c_float),
         ("samplesPerIteration", ctypes.c_int), ("agent", ctypes.c_int), ("fixGNewClear", ctypes.c_int),
-        ("device", ctypes.c_int), ("profileKernels", ctypes.c_int),
+        ("device", ctypes.c_int), ("profileKernels", ctypes.c_int), ("batchRule", ctypes.c_int),
     ]
 
 
@@ -64,7 +66,7 @@ EXPORTED_SYMBOLS = (
     "sbmp_kgmt_enqueue", "sbmp_kgmt_sync", "sbmp_kgmt_result", "sbmp_kgmt_stream", "sbmp_kgmt_copy_tree",
     "sbmp_kgmt_copy_unexplored", "sbmp_kgmt_copy_flags", "sbmp_kgmt_copy_regions", "sbmp_kgmt_num_slots",
     "sbmp_kgmt_copy_rng", "sbmp_kgmt_iter_log", "sbmp_kgmt_export_csv", "sbmp_kgmt_kernel_stats",
-    "sbmp_kgmt_reset_kernel_stats", "sbmp_read_obstacles_csv", "sbmp_device_upload_f32", "sbmp_device_free",
+    "sbmp_kgmt_reset_kernel_stats", "sbmp_kgmt_set_profiling", "sbmp_read_obstacles_csv", "sbmp_device_upload_f32", "sbmp_device_free",
     "sbmp_device_count", "sbmp_comm_get_unique_id", "sbmp_kgmt_create_sharded",
 )
 
@@ -112,6 +114,7 @@ def lib():
         "sbmp_kgmt_export_csv": [vp, ctypes.c_char_p],
         "sbmp_kgmt_kernel_stats": [vp, vp, i, P(i)],
         "sbmp_kgmt_reset_kernel_stats": [vp],
+        "sbmp_kgmt_set_profiling": [vp, i],
         "sbmp_read_obstacles_csv": [ctypes.c_char_p, i, vp, i, P(i)],
         "sbmp_device_upload_f32": [vp, ctypes.c_size_t, P(vp)],
         "sbmp_device_free": [vp],

@@ -48,11 +48,14 @@ struct PlannerStatus {
     int pad[15];
 };
 
+constexpr int kMaxLdsObs = 2048;     // obstacle lists up to 32 KB are staged in LDS per block
+
 // Everything a kernel needs, passed by value.
 struct KgmtDev {
-    int M, nSlots, nWords, numIterations, numDisc, N, n, nR1, nR2, nObs, cap, fixGNewClear;
+    int M, nSlots, nWords, nBlocks, numIterations, numDisc, N, n, nR1, nR2, nObs, cap, fixGNewClear;
+    int batchRule;        // 0 = reference rule (+ cap), 1 = fill the cap (D14)
     int nranks, rank;
-    float width, height, agentLength, goalThreshold, R1Size, R2Size, goalX, goalY;
+    float width, height, agentLength, invAgentLength, goalThreshold, R1Size, R2Size, goalX, goalY;
     float4* treeState;
     float4* treeCtrl;
     int* treeParent;
@@ -61,7 +64,8 @@ struct KgmtDev {
     uint4* rngA;
     uint2* rngB;
     unsigned long long* gnew;
-    int* wordOffsets;
+    int* blockCount;      // GNew popcount per 256-slot block (written by k_expand)
+    int* blockOffsets;    // exclusive prefix of blockCount (written by k_plan)
     int* R1;
     int* R1Avail;
     int* R1Valid;
@@ -69,10 +73,11 @@ struct KgmtDev {
     int* R1Cov;           // available R2 cells per R1 cell (covR numerator, kept incrementally)
     uint32_t* R2Avail;    // live availability bits
     uint32_t* R2Snap;     // availability bits at the iteration start (D2)
+    uint32_t* R2New;      // cells seen valid this iteration while unavailable in the snapshot
     int* R2Valid;
     int* R2Invalid;
     float* R1Score;       // [2][nR1]
-    int* delta;           // [4*nR1 + nR2]: R1, R1Valid, R1Invalid, R1AvailSet, R2AvailSet
+    int* delta;           // [4*nR1]: R1, R1Valid, R1Invalid, R1AvailSet of this iteration
     const float4* obstacles;
     IterCtrl* ctrl;
     PlannerStatus* status;
@@ -129,10 +134,24 @@ SBMP_HD float xorwow_uniform(Xorwow& s) {
 // ---------------------------------------------------------------- collision
 // reference collisionCheck.cu:6-28: a segment AABB is free of an obstacle box
 // iff separated on some axis; the motion is valid iff free of every box.
+// OBS_LDS: the list is staged in LDS and every box is tested without early
+// exit (independent broadcast reads, no load->compare->branch chain; the result
+// is an order-independent OR, so identical to the reference's early return).
+// Otherwise the list is read from global memory with the reference's early exit.
+template <bool OBS_LDS>
 __device__ __forceinline__ bool motion_valid(float minx, float miny, float maxx, float maxy,
                                              const float4* __restrict__ obs, int nObs) {
+    if (OBS_LDS) {
+        bool hit = false;
+#pragma unroll 4
+        for (int i = 0; i < nObs; ++i) {
+            const float4 o = obs[i];   // (xmin, ymin, xmax, ymax)
+            hit |= !((maxx <= o.x) || (o.z <= minx) || (maxy <= o.y) || (o.w <= miny));
+        }
+        return !hit;
+    }
     for (int i = 0; i < nObs; ++i) {
-        const float4 o = obs[i];   // (xmin, ymin, xmax, ymax)
+        const float4 o = obs[i];
         const bool free_ = (maxx <= o.x) || (o.z <= minx) || (maxy <= o.y) || (o.w <= miny);
         if (!free_) return false;
     }
@@ -146,7 +165,12 @@ struct ChildOut {
 
 // reference statePropagator.cu:5-76 (car).  Same operation sequence as the oracle
 // (D9-D11): fmaf where nvcc would contract, steering via one double fma.
-__device__ __forceinline__ bool propagate_car(float4 p, Xorwow& rs, const KgmtDev& d, ChildOut& out) {
+// v / agentLength: when agentLength is a power of two, v * (1/agentLength) is the
+// same correctly rounded value (both are the exact product scaled by 2^-k), so the
+// host passes invAgentLength != 0 and the per-step division disappears.
+template <bool OBS_LDS>
+__device__ __forceinline__ bool propagate_car(float4 p, Xorwow& rs, const KgmtDev& d, const float4* obs,
+                                              ChildOut& out) {
     const float a = __builtin_fmaf(xorwow_uniform(rs), 10.0f, -5.0f);
     const float u2 = xorwow_uniform(rs);
     const float steering = (float)__builtin_fma((double)(u2 * 2.0f), 3.141592653589793, -3.141592653589793);
@@ -165,11 +189,12 @@ __device__ __forceinline__ bool propagate_car(float4 p, Xorwow& rs, const KgmtDe
             valid = false;
             break;
         }
-        theta = __builtin_fmaf((v / d.agentLength) * tan_steering, dt, theta);
+        const float vl = (d.invAgentLength != 0.0f) ? v * d.invAgentLength : v / d.agentLength;
+        theta = __builtin_fmaf(vl * tan_steering, dt, theta);
         v = __builtin_fmaf(a, dt, v);
         const float minx = (px > x) ? x : px, maxx = (px > x) ? px : x;
         const float miny = (py > y) ? y : py, maxy = (py > y) ? py : y;
-        if (!motion_valid(minx, miny, maxx, maxy, d.obstacles, d.nObs)) {
+        if (!motion_valid<OBS_LDS>(minx, miny, maxx, maxy, obs, d.nObs)) {
             valid = false;
             break;
         }
@@ -182,7 +207,9 @@ __device__ __forceinline__ bool propagate_car(float4 p, Xorwow& rs, const KgmtDe
 }
 
 // Holonomic R2 point (build extension).
-__device__ __forceinline__ bool propagate_point(float4 p, Xorwow& rs, const KgmtDev& d, ChildOut& out) {
+template <bool OBS_LDS>
+__device__ __forceinline__ bool propagate_point(float4 p, Xorwow& rs, const KgmtDev& d, const float4* obs,
+                                                ChildOut& out) {
     const float vx = __builtin_fmaf(xorwow_uniform(rs), 2.0f, -1.0f);
     const float vy = __builtin_fmaf(xorwow_uniform(rs), 2.0f, -1.0f);
     const float duration = __builtin_fmaf(xorwow_uniform(rs), 1.0f, 0.05f);
@@ -199,7 +226,7 @@ __device__ __forceinline__ bool propagate_point(float4 p, Xorwow& rs, const Kgmt
         }
         const float minx = (px > x) ? x : px, maxx = (px > x) ? px : x;
         const float miny = (py > y) ? y : py, maxy = (py > y) ? py : y;
-        if (!motion_valid(minx, miny, maxx, maxy, d.obstacles, d.nObs)) {
+        if (!motion_valid<OBS_LDS>(minx, miny, maxx, maxy, obs, d.nObs)) {
             valid = false;
             break;
         }

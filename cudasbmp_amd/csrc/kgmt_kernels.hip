@@ -1,17 +1,19 @@
 // kgmt_kernels.hip — hand-written gfx950 kernels of the KGMT iteration.
 //
-// One reference iteration (reference src/planners/KGMT.cu:118-292) becomes three
+// One reference iteration (reference src/planners/KGMT.cu:118-292) becomes two
 // kernels on one stream, with no host round trip:
 //   k_expand(t)  : propagateG / propagateGV2 (KGMT.cu:341-482) fused with
 //                  propagateAndCheck + isMotionValid (statePropagator.cu:5-76,
 //                  collisionCheck.cu:6-28), region binning and the accept test.
-//                  One thread per child slot, wave64 ballot -> GNew bitmask.
-//   k_plan(t+1)  : exclusive_scan(GNew) (KGMT.cu:222-224) as a popcount scan of
-//                  the bitmask, application of this iteration's region deltas,
-//                  the next iteration's frontier/batch decision (KGMT.cu:139-188)
-//                  and updateR1 (KGMT.cu:485-538).  One 1024-thread workgroup.
-//   k_insert(t)  : findInd + updateG (KGMT.cu:225-245,540-593): append accepted
-//                  children in slot order, goal test, partial GNew clear (D6).
+//                  One thread per child slot, wave64 ballot -> GNew bitmask and a
+//                  GNew popcount per 256-slot block.
+//   k_finish(t)  : blocks 1..: exclusive_scan(GNew) + findInd + updateG
+//                  (KGMT.cu:222-245,540-593) — each block sums the popcounts of
+//                  the blocks before it, appends its accepted children in slot
+//                  order, tests the goal and applies the partial GNew clear (D6);
+//                  block 0, concurrently: folds the region deltas and prepares
+//                  iteration t+1 (frontier/batch decision KGMT.cu:139-188,
+//                  updateR1 KGMT.cu:485-538).
 // The reference's O(M) G scan + findInd disappears: every frontier node is
 // expanded each iteration and new rows are appended contiguously, so G is
 // always the row range [gLo, treeSize) (parity-tested against the oracle,
@@ -28,18 +30,75 @@
 namespace sbmp {
 
 // ------------------------------------------------------------------ expand
-template <int AGENT>
+
+// ------------------------------------------------------------------ helpers
+__device__ __forceinline__ int wave_sum(int v) {
+#pragma unroll
+    for (int off = kWave / 2; off > 0; off >>= 1) v += __shfl_xor(v, off, kWave);
+    return v;
+}
+
+// Sum of counts[0, nb) and of counts[0, mine) over a 256-thread block.  counts is
+// allocated with a multiple-of-4 length and zero beyond every written entry.
+__device__ __forceinline__ void block_prefix_total(const int* __restrict__ counts, int nb, int mine, int* pre,
+                                                   int* tot, int (*sRed)[kBlock / kWave]) {
+    int p = 0, s = 0;
+    const int nb4 = (nb + 3) & ~3;
+    for (int i = threadIdx.x * 4; i < nb4; i += kBlock * 4) {
+        const int4 v = *reinterpret_cast<const int4*>(counts + i);
+        s += v.x + v.y + v.z + v.w;
+        p += (i < mine ? v.x : 0) + (i + 1 < mine ? v.y : 0) + (i + 2 < mine ? v.z : 0) + (i + 3 < mine ? v.w : 0);
+    }
+    p = wave_sum(p);
+    s = wave_sum(s);
+    const int wave = threadIdx.x >> 6;
+    if ((threadIdx.x & (kWave - 1)) == 0) {
+        sRed[0][wave] = p;
+        sRed[1][wave] = s;
+    }
+    __syncthreads();
+    *pre = sRed[0][0] + sRed[0][1] + sRed[0][2] + sRed[0][3];
+    *tot = sRed[1][0] + sRed[1][1] + sRed[1][2] + sRed[1][3];
+}
+
+// ------------------------------------------------------------------ expand
+// One thread per child slot; one 256-thread block per 256-slot ownership block.
+// Outputs: child state/controls/parent (2 x 16 B), XORWOW state (16 + 8 B),
+// GNew bits (one 8-B word per wave), the block's GNew popcount, block-private
+// R1 counters flushed once per block, R2 valid/invalid counters aggregated per
+// (cell, validity) in an LDS hash table and flushed once per distinct key, and
+// R2New bits for cells that were unavailable in the iteration-start snapshot.
+constexpr int kHash = 512;
+
+template <int AGENT, bool OBS_LDS>
 __global__ __launch_bounds__(kBlock) void k_expand(KgmtDev d, int t) {
+    extern __shared__ float4 sObs[];
     __shared__ float sScore[kMaxR1];
     __shared__ int sCnt[4][kMaxR1];   // R1, R1Valid, R1Invalid, R1AvailSet (block-private)
+    __shared__ int sKey[kHash];       // (r2 << 1 | valid) -> count
+    __shared__ int sVal[kHash];
+    __shared__ int sWaveCnt[kBlock / kWave];
 
     const IterCtrl c = d.ctrl[t];
     if (!c.run || d.status->goalIdx != kNoGoal) return;   // grid-uniform
+    if (blockIdx.x == 0 && threadIdx.x == 0) d.ctrl[t].executed = 1;
     const int gblock = d.rank + d.nranks * (int)blockIdx.x;  // block-cyclic slot ownership
     const int slotBase = gblock * kBlock;
-    if (slotBase >= c.S) return;                           // block-uniform
-
     const int tid = threadIdx.x;
+    const int lane = tid & (kWave - 1);
+    const int wave = tid >> 6;
+
+    if (slotBase >= c.S) {
+        // Past this iteration's batch: publish the stale GNew bits' count (D6) so the
+        // compaction sees them; nothing else to do.
+        if (slotBase < c.H) {
+            if (lane == 0) sWaveCnt[wave] = __popcll(d.gnew[(slotBase >> 6) + wave]);
+            __syncthreads();
+            if (tid == 0) d.blockCount[gblock] = sWaveCnt[0] + sWaveCnt[1] + sWaveCnt[2] + sWaveCnt[3];
+        }
+        return;
+    }
+
     const float* score = d.R1Score + c.scoreBuf * d.nR1;
     for (int i = tid; i < d.nR1; i += kBlock) {
         sScore[i] = score[i];
@@ -48,7 +107,14 @@ __global__ __launch_bounds__(kBlock) void k_expand(KgmtDev d, int t) {
         sCnt[2][i] = 0;
         sCnt[3][i] = 0;
     }
+    for (int i = tid; i < kHash; i += kBlock) {
+        sKey[i] = -1;
+        sVal[i] = 0;
+    }
+    if (OBS_LDS)
+        for (int i = tid; i < d.nObs; i += kBlock) sObs[i] = d.obstacles[i];
     __syncthreads();
+    const float4* obs = OBS_LDS ? sObs : d.obstacles;
 
     const int slot = slotBase + tid;
     bool accept = false;
@@ -60,7 +126,8 @@ __global__ __launch_bounds__(kBlock) void k_expand(KgmtDev d, int t) {
         const uint2 rb = d.rngB[slot];
         Xorwow rs{ra.x, ra.y, ra.z, ra.w, rb.x, rb.y};
         ChildOut ch;
-        const bool valid = (AGENT == 0) ? propagate_car(p, rs, d, ch) : propagate_point(p, rs, d, ch);
+        const bool valid = (AGENT == 0) ? propagate_car<OBS_LDS>(p, rs, d, obs, ch)
+                                        : propagate_point<OBS_LDS>(p, rs, d, obs, ch);
         const int r1 = getR1(ch.state.x, ch.state.y, d.R1Size, d.N);
         const int r2 = getR2(ch.state.x, ch.state.y, r1, d.R1Size, d.N, d.R2Size, d.n);
         if (valid) {
@@ -68,7 +135,6 @@ __global__ __launch_bounds__(kBlock) void k_expand(KgmtDev d, int t) {
             if (r1 >= 0 && r2 >= 0) {
                 const bool r2Avail = (d.R2Snap[r2 >> 5] >> (r2 & 31)) & 1u;
                 accept = (u <= sScore[r1]) || !r2Avail;
-                if (!r2Avail) d.delta[4 * d.nR1 + r2] = 1;   // idempotent plain store
             }
         }
         // Region counters (KGMT.cu:392-411; D3: in-grid cells only).
@@ -81,7 +147,18 @@ __global__ __launch_bounds__(kBlock) void k_expand(KgmtDev d, int t) {
                 atomicAdd(&sCnt[2][r1], 1);
             }
         }
-        if (r2 >= 0) atomicAdd(valid ? &d.R2Valid[r2] : &d.R2Invalid[r2], 1);
+        if (r2 >= 0) {
+            const int key = (r2 << 1) | (valid ? 1 : 0);
+            uint32_t h = ((uint32_t)key * 2654435761u) >> 23;   // 9 bits
+            while (true) {
+                const int old = atomicCAS(&sKey[h], -1, key);
+                if (old == -1 || old == key) {
+                    atomicAdd(&sVal[h], 1);
+                    break;
+                }
+                h = (h + 1) & (kHash - 1);
+            }
+        }
 
         d.uState[slot] = ch.state;
         d.uCtrl[slot] = make_float4(ch.a, ch.steer, ch.dur, __int_as_float(parent));
@@ -90,166 +167,151 @@ __global__ __launch_bounds__(kBlock) void k_expand(KgmtDev d, int t) {
     }
     // GNew |= accept (stale bits survive, D6).  A wave covers one 64-bit word.
     const unsigned long long mask = __ballot(accept);
-    if ((tid & (kWave - 1)) == 0 && mask) d.gnew[slot >> 6] |= mask;
-
+    if (lane == 0) {
+        const unsigned long long old = d.gnew[slot >> 6];
+        const unsigned long long now = old | mask;
+        if (now != old) d.gnew[slot >> 6] = now;
+        sWaveCnt[wave] = __popcll(now);
+    }
     __syncthreads();
+    if (tid == 0) d.blockCount[gblock] = sWaveCnt[0] + sWaveCnt[1] + sWaveCnt[2] + sWaveCnt[3];
     for (int i = tid; i < d.nR1; i += kBlock) {
         if (sCnt[0][i]) atomicAdd(&d.delta[i], sCnt[0][i]);
         if (sCnt[1][i]) atomicAdd(&d.delta[d.nR1 + i], sCnt[1][i]);
         if (sCnt[2][i]) atomicAdd(&d.delta[2 * d.nR1 + i], sCnt[2][i]);
         if (sCnt[3][i]) d.delta[3 * d.nR1 + i] = 1;
     }
-}
-
-// ------------------------------------------------------------------ plan
-// Block-wide exclusive scan of one int per thread (1024 threads = 16 waves).
-__device__ __forceinline__ int block_exclusive_scan(int v, int* sWave, int* total) {
-    const int lane = threadIdx.x & (kWave - 1);
-    const int wave = threadIdx.x >> 6;
-    int x = v;
-#pragma unroll
-    for (int off = 1; off < kWave; off <<= 1) {
-        const int y = __shfl_up(x, off, kWave);
-        if (lane >= off) x += y;
-    }
-    if (lane == kWave - 1) sWave[wave] = x;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        int run = 0;
-        for (int w = 0; w < (int)(blockDim.x >> 6); ++w) {
-            const int s = sWave[w];
-            sWave[w] = run;
-            run += s;
+    for (int i = tid; i < kHash; i += kBlock) {
+        const int key = sKey[i];
+        if (key < 0) continue;
+        const int r2 = key >> 1;
+        if (key & 1) {
+            atomicAdd(&d.R2Valid[r2], sVal[i]);
+            const uint32_t bit = 1u << (r2 & 31);
+            if (!(d.R2Snap[r2 >> 5] & bit)) atomicOr(&d.R2New[r2 >> 5], bit);
+        } else {
+            atomicAdd(&d.R2Invalid[r2], sVal[i]);
         }
-        sWave[16] = run;
     }
-    __syncthreads();
-    *total = sWave[16];
-    return sWave[wave] + x - v;
 }
 
-__global__ __launch_bounds__(1024) void k_plan(KgmtDev d, int t) {
-    __shared__ int sWave[17];
+// ------------------------------------------------------------------ finish
+// Batch decision for iteration t (KGMT.cu:151-158 + the capped / fill extensions).
+__device__ __forceinline__ void batch_rule(const KgmtDev& d, int treeSize, int nG, int* k, int* nExp) {
+    *k = 0;
+    *nExp = 0;
+    if (nG <= 0) return;   // D7: a zero-block launch is a no-op
+    long long remaining = (long long)d.M - treeSize;
+    if (d.cap > 0 && remaining > d.cap) remaining = d.cap;
+    if (d.cap > 0 && d.batchRule == 1) {   // D14: fill the batch
+        if (nG <= remaining) {
+            *k = (int)(remaining / nG);
+            *nExp = nG;
+        } else {
+            *k = 1;
+            *nExp = (int)remaining;
+        }
+    } else if (32ll * nG <= remaining) {
+        *k = 32;
+        *nExp = nG;
+    } else {
+        *k = (int)((float)remaining / (float)nG);   // KGMT.cu:157
+        *nExp = nG;
+        if (d.cap > 0 && *k == 0) {
+            *k = 1;
+            *nExp = (int)remaining;
+        }
+    }
+}
+
+// Close iteration t-1 (accepted count, region deltas) and prepare iteration t:
+// frontier range, batch, updateR1 (KGMT.cu:485-538), availability snapshot.
+// Runs in block 0 of k_finish(t-1), concurrently with that launch's insert blocks
+// (it reads only what k_expand(t-1) wrote and nothing the insert blocks write).
+__device__ void plan_iteration(const KgmtDev& d, int t) {
+    __shared__ int sRed[2][kBlock / kWave];
     __shared__ int sCovInc[kMaxR1];
     __shared__ float sScore[kMaxR1];
     __shared__ float sPart[8];
 
     const int tid = threadIdx.x;
-    bool ranPrev = false;
-    if (t > 1) ranPrev = d.ctrl[t - 1].run && d.status->goalIdx == kNoGoal;
+    const bool ranPrev = (t > 1) && d.ctrl[t - 1].executed;
     if (t > 1 && !ranPrev) {
         if (tid == 0) d.ctrl[t].run = 0;
         return;
     }
-
     int treeSize = 1, gLo = 0, H = 0, A = 0;
     IterCtrl pc;
     if (ranPrev) {
         pc = d.ctrl[t - 1];
         H = pc.H;
-        // (1) exclusive_scan(GNew) over [0, H): popcounts of the bitmask words.
-        const int nw = (H + 63) >> 6;
-        const int per = (nw + (int)blockDim.x - 1) / (int)blockDim.x;
-        const int w0 = min(nw, tid * per), w1 = min(nw, w0 + per);
-        int cnt = 0;
-        for (int w = w0; w < w1; ++w) cnt += __popcll(d.gnew[w]);
-        int run = block_exclusive_scan(cnt, sWave, &A);
-        for (int w = w0; w < w1; ++w) {
-            d.wordOffsets[w] = run;
-            run += __popcll(d.gnew[w]);
-        }
+        int pre;
+        block_prefix_total(d.blockCount, (H + kBlock - 1) / kBlock, 0, &pre, &A, sRed);
     }
-    {
-        // (2) fold the previous expansion's region deltas into the tables and take
-        // the availability snapshot for iteration t (t == 1: deltas are zero).
-        if (tid < kMaxR1) sCovInc[tid] = 0;
-        for (int i = tid; i < d.nR1; i += blockDim.x) {
-            int* dl = d.delta;
-            const int a0 = dl[i], a1 = dl[d.nR1 + i], a2 = dl[2 * d.nR1 + i], a3 = dl[3 * d.nR1 + i];
-            if (a0) { d.R1[i] += a0; dl[i] = 0; }
-            if (a1) { d.R1Valid[i] += a1; dl[d.nR1 + i] = 0; }
-            if (a2) { d.R1Invalid[i] += a2; dl[2 * d.nR1 + i] = 0; }
-            if (a3) { d.R1Avail[i] = 1; dl[3 * d.nR1 + i] = 0; }
-        }
-        __syncthreads();
-        const int nn = d.n * d.n;
-        const int nR2w = d.nR2 >> 5;
-        for (int w = tid; w < nR2w; w += blockDim.x) {   // one thread owns one availability word
-            int4* dl = reinterpret_cast<int4*>(d.delta + 4 * d.nR1 + 32 * w);
-            uint32_t bits = d.R2Avail[w];
-            const uint32_t old = bits;
-#pragma unroll
-            for (int q = 0; q < 8; ++q) {
-                const int4 v = dl[q];
-                if (v.x | v.y | v.z | v.w) {
-                    const int c0 = 32 * w + 4 * q;
-                    const int vv[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-                    for (int e = 0; e < 4; ++e) {
-                        const uint32_t b = 1u << (4 * q + e);
-                        if (vv[e] && !(bits & b)) {
-                            bits |= b;
-                            atomicAdd(&sCovInc[(c0 + e) / nn], 1);
-                        }
-                    }
-                    dl[q] = make_int4(0, 0, 0, 0);
+    // Fold the previous expansion's region deltas into the tables and take the
+    // availability snapshot for iteration t (t == 1: nothing to fold).
+    for (int i = tid; i < kMaxR1; i += kBlock) sCovInc[i] = 0;
+    for (int i = tid; i < d.nR1; i += kBlock) {
+        int* dl = d.delta;
+        const int a0 = dl[i], a1 = dl[d.nR1 + i], a2 = dl[2 * d.nR1 + i], a3 = dl[3 * d.nR1 + i];
+        if (a0) { d.R1[i] += a0; dl[i] = 0; }
+        if (a1) { d.R1Valid[i] += a1; dl[d.nR1 + i] = 0; }
+        if (a2) { d.R1Invalid[i] += a2; dl[2 * d.nR1 + i] = 0; }
+        if (a3) { d.R1Avail[i] = 1; dl[3 * d.nR1 + i] = 0; }
+    }
+    __syncthreads();
+    const int nn = d.n * d.n;
+    const int nR2w = d.nR2 >> 5;
+    for (int w = tid; w < nR2w; w += kBlock) {   // one thread owns one availability word
+        uint32_t bits = d.R2Avail[w];
+        const uint32_t nw = d.R2New[w];
+        if (nw) {
+            d.R2New[w] = 0u;
+            uint32_t fresh = nw & ~bits;
+            if (fresh) {
+                bits |= fresh;
+                d.R2Avail[w] = bits;
+                while (fresh) {
+                    const int b = __builtin_ctz(fresh);
+                    fresh &= fresh - 1u;
+                    atomicAdd(&sCovInc[(32 * w + b) / nn], 1);
                 }
             }
-            if (bits != old) d.R2Avail[w] = bits;
-            d.R2Snap[w] = bits;   // snapshot for the next expand (D2)
         }
-        __syncthreads();
-        if (tid < d.nR1 && sCovInc[tid]) d.R1Cov[tid] += sCovInc[tid];
+        d.R2Snap[w] = bits;   // snapshot for the next expand (D2)
     }
+    __syncthreads();
+    for (int i = tid; i < d.nR1; i += kBlock)
+        if (sCovInc[i]) d.R1Cov[i] += sCovInc[i];
     if (ranPrev) {
-        treeSize = pc.treeSize + A;
+        treeSize = pc.treeSize + A;   // KGMT.cu:249
         gLo = pc.gLo + pc.nExp;
-        if (tid == 0) {
-            d.ctrl[t - 1].executed = 1;
-            d.ctrl[t - 1].A = A;
-        }
+        if (tid == 0) d.ctrl[t - 1].A = A;
     }
 
-    // (3) next iteration's frontier / batch decision (KGMT.cu:151-158 + capped extension).
-    const int run_t = (t <= d.numIterations) && (treeSize < d.M);
+    const int run_t = (t <= d.numIterations) && (treeSize < d.M);   // KGMT.cu:118,255
     int nG = 0, k = 0, nExp = 0;
     if (run_t) {
         nG = treeSize - gLo;
-        if (nG > 0) {
-            long long remaining = (long long)d.M - treeSize;
-            if (d.cap > 0 && remaining > d.cap) remaining = d.cap;
-            if (32ll * nG <= remaining) {
-                k = 32;
-                nExp = nG;
-            } else {
-                k = (int)((float)remaining / (float)nG);   // KGMT.cu:157
-                nExp = nG;
-                if (d.cap > 0 && k == 0) {
-                    k = 1;
-                    nExp = (int)remaining;
-                }
-            }
-        }
+        batch_rule(d, treeSize, nG, &k, &nExp);
     }
     const int S = k * nExp;
     const int buf = t & 1;
-
-    // (4) updateR1 (KGMT.cu:485-538) for iteration t.
-    if (run_t) {
+    if (run_t) {   // updateR1 for iteration t
         __syncthreads();
-        if (tid < d.nR1) {
+        for (int i = tid; i < d.nR1; i += kBlock) {
             float s = 0.0f;
-            if (d.R1Avail[tid] != 0) {
-                const int nValid = d.R1Valid[tid];
-                const float covR = (float)d.R1Cov[tid] / (float)(d.n * d.n);
-                const float freeVol = (0.01f + (float)nValid) / (0.01f + (float)nValid + (float)d.R1Invalid[tid]);
+            if (d.R1Avail[i] != 0) {
+                const int nValid = d.R1Valid[i];
+                const float covR = (float)d.R1Cov[i] / (float)nn;
+                const float freeVol = (0.01f + (float)nValid) / (0.01f + (float)nValid + (float)d.R1Invalid[i]);
                 const float fv2 = freeVol * freeVol;
                 const float fv4 = fv2 * fv2;
-                const double r = (double)d.R1[tid];
+                const double r = (double)d.R1[i];
                 const double den = (double)(1.0f + covR) * (1.0 + r * r);
                 s = (float)((double)fv4 / den);
             }
-            sScore[tid] = s;
+            sScore[i] = s;
         }
         __syncthreads();
         if (tid < 8) {   // CUB BlockReduce order (D8): balanced tree per 32 group ...
@@ -270,10 +332,9 @@ __global__ __launch_bounds__(1024) void k_plan(KgmtDev d, int t) {
             sPart[0] = total;
         }
         __syncthreads();
-        if (tid < d.nR1) {
-            const float total = sPart[0];
-            d.R1Score[buf * d.nR1 + tid] = (d.R1Avail[tid] == 0) ? 1.0f : sScore[tid] / total;
-        }
+        const float total = sPart[0];
+        for (int i = tid; i < d.nR1; i += kBlock)
+            d.R1Score[buf * d.nR1 + i] = (d.R1Avail[i] == 0) ? 1.0f : sScore[i] / total;
     }
     if (tid == 0) {
         IterCtrl c;
@@ -293,22 +354,35 @@ __global__ __launch_bounds__(1024) void k_plan(KgmtDev d, int t) {
     }
 }
 
-// ------------------------------------------------------------------ insert
-__global__ __launch_bounds__(kBlock) void k_insert(KgmtDev d, int t) {
+// One 256-slot block of iteration t: the j-th accepted slot (global slot order)
+// becomes row treeSize + j (findInd + updateG, KGMT.cu:225-245,540-593), goal test,
+// partial GNew clear (D6).  The block's j offset is the sum of the GNew counts of
+// the blocks before it (counts written by k_expand(t)).
+__device__ void insert_block(const KgmtDev& d, int t, int gblock) {
+    __shared__ int sRed[2][kBlock / kWave];
+    __shared__ int sWaveCnt[kBlock / kWave];
     const IterCtrl c = d.ctrl[t];
     if (!c.executed) return;
+    if (gblock * kBlock >= c.H) return;
+    if (d.blockCount[gblock] == 0) return;   // no accepted (or stale) slot: nothing to insert or clear
+    int pre, A;
+    block_prefix_total(d.blockCount, (c.H + kBlock - 1) / kBlock, gblock, &pre, &A, sRed);
+
     const int lane = threadIdx.x & (kWave - 1);
-    const int w = blockIdx.x * (kBlock / kWave) + (threadIdx.x >> 6);
-    const int nw = (c.H + 63) >> 6;
-    if (w >= nw) return;
+    const int wave = threadIdx.x >> 6;
+    const int w = gblock * (kBlock / kWave) + wave;
     const unsigned long long word = d.gnew[w];
+    if (lane == 0) sWaveCnt[wave] = __popcll(word);
+    __syncthreads();
+    int waveOff = pre;
+    for (int i = 0; i < wave; ++i) waveOff += sWaveCnt[i];
     if (word == 0ull) return;
 
     const int m32 = d.M / 32;
-    const int grid = min(c.A, m32);   // updateG launch: min(|GNew|, M/32) blocks of 32 (KGMT.cu:231)
-    const int nIns = 32 * grid < c.A ? 32 * grid : c.A;
+    const int grid = min(A, m32);   // updateG launch: min(|GNew|, M/32) blocks of 32 (KGMT.cu:231)
+    const int nIns = 32 * grid < A ? 32 * grid : A;
     if ((word >> lane) & 1ull) {
-        const int j = d.wordOffsets[w] + __popcll(word & ((1ull << lane) - 1ull));
+        const int j = waveOff + __popcll(word & ((1ull << lane) - 1ull));
         const int dst = c.treeSize + j;
         if (j < nIns && dst < d.M) {   // D13: the reference writes past M here
             const int slot = w * kWave + lane;
@@ -332,6 +406,15 @@ __global__ __launch_bounds__(kBlock) void k_insert(KgmtDev d, int t) {
         else if (base < cleared) nw_ = word & ~((1ull << (cleared - base)) - 1ull);
         if (nw_ != word) d.gnew[w] = nw_;
     }
+}
+
+// k_finish(t): block 0 prepares iteration t+1, blocks 1.. insert iteration t.
+__global__ __launch_bounds__(kBlock) void k_finish(KgmtDev d, int t) {
+    if (blockIdx.x == 0) {
+        plan_iteration(d, t + 1);
+        return;
+    }
+    insert_block(d, t, d.rank + d.nranks * ((int)blockIdx.x - 1));
 }
 
 // ------------------------------------------------------------------ init
@@ -419,20 +502,20 @@ __global__ void k_export_unexplored(KgmtDev d, float* samples, int* uParent) {
 
 // ------------------------------------------------------------------ launchers
 void launch_expand(const KgmtDev& d, int t, int agent, int blocks, hipStream_t s) {
-    if (agent == 0)
-        hipLaunchKernelGGL(k_expand<0>, dim3(blocks), dim3(kBlock), 0, s, d, t);
-    else
-        hipLaunchKernelGGL(k_expand<1>, dim3(blocks), dim3(kBlock), 0, s, d, t);
+    const bool lds = d.nObs <= kMaxLdsObs;
+    const size_t shm = lds ? sizeof(float4) * (size_t)d.nObs : 0;
+    if (agent == 0) {
+        if (lds) hipLaunchKernelGGL((k_expand<0, true>), dim3(blocks), dim3(kBlock), shm, s, d, t);
+        else hipLaunchKernelGGL((k_expand<0, false>), dim3(blocks), dim3(kBlock), 0, s, d, t);
+    } else {
+        if (lds) hipLaunchKernelGGL((k_expand<1, true>), dim3(blocks), dim3(kBlock), shm, s, d, t);
+        else hipLaunchKernelGGL((k_expand<1, false>), dim3(blocks), dim3(kBlock), 0, s, d, t);
+    }
 }
 
-void launch_plan(const KgmtDev& d, int t, hipStream_t s) {
-    hipLaunchKernelGGL(k_plan, dim3(1), dim3(1024), 0, s, d, t);
+void launch_finish(const KgmtDev& d, int t, int insertBlocks, hipStream_t s) {
+    hipLaunchKernelGGL(k_finish, dim3(1 + insertBlocks), dim3(kBlock), 0, s, d, t);
 }
-
-void launch_insert(const KgmtDev& d, int t, int blocks, hipStream_t s) {
-    hipLaunchKernelGGL(k_insert, dim3(blocks), dim3(kBlock), 0, s, d, t);
-}
-
 void launch_fill_i32(int* p, int v, long long n, hipStream_t s) {
     if (n <= 0) return;
     const int blocks = (int)std::min<long long>((n + 255) / 256, 4096);

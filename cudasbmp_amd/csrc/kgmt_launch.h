@@ -11,8 +11,9 @@
 namespace sbmp {
 
 void launch_expand(const KgmtDev& d, int t, int agent, int blocks, hipStream_t s);
-void launch_plan(const KgmtDev& d, int t, hipStream_t s);
-void launch_insert(const KgmtDev& d, int t, int blocks, hipStream_t s);
+// k_finish(t): insert iteration t (insertBlocks blocks) + prepare iteration t+1.
+// t = 0 prepares iteration 1 only (insertBlocks = 0).
+void launch_finish(const KgmtDev& d, int t, int insertBlocks, hipStream_t s);
 void launch_fill_i32(int* p, int v, long long n, hipStream_t s);
 void launch_fill_f32(float* p, float v, long long n, hipStream_t s);
 void launch_init_slots(const KgmtDev& d, const Xorwow& base, const uint32_t* jumps, int nbits, int blocks,

@@ -9,6 +9,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <cmath>
 #include <cstring>
 #include <fstream>
 #include <iomanip>
@@ -44,6 +45,10 @@ KgmtPlanner::KgmtPlanner(const sbmp_kgmt_params& p, int nranks, int rank, Exchan
     if (p.numDisc < 1) throw Error(SBMP_ERR_INVALID_ARGUMENT, "numDisc must be >= 1");
     if (p.numIterations < 0) throw Error(SBMP_ERR_INVALID_ARGUMENT, "numIterations must be >= 0");
     if (p.samplesPerIteration < 0) throw Error(SBMP_ERR_INVALID_ARGUMENT, "samplesPerIteration must be >= 0");
+    if (p.batchRule != SBMP_BATCH_REFERENCE && p.batchRule != SBMP_BATCH_FILL)
+        throw Error(SBMP_ERR_INVALID_ARGUMENT, "unknown batchRule");
+    if (p.batchRule == SBMP_BATCH_FILL && p.samplesPerIteration <= 0)
+        throw Error(SBMP_ERR_INVALID_ARGUMENT, "batchRule FILL needs samplesPerIteration > 0");
     if (p.agent != SBMP_AGENT_CAR && p.agent != SBMP_AGENT_POINT) throw Error(SBMP_ERR_INVALID_ARGUMENT, "unknown agent");
     if (!(p.width > 0.0f) || !(p.height > 0.0f)) throw Error(SBMP_ERR_INVALID_ARGUMENT, "width/height must be > 0");
     if (nranks < 1 || rank < 0 || rank >= nranks) throw Error(SBMP_ERR_INVALID_ARGUMENT, "bad rank/nranks");
@@ -58,13 +63,14 @@ KgmtPlanner::KgmtPlanner(const sbmp_kgmt_params& p, int nranks, int rank, Exchan
     slotsPadded_ = round_up(nSlots, (long long)kBlock * nranks);
     expandBlocks_ = slotsPadded_ / kBlock / nranks;
     const int nWords = slotsPadded_ / kWave;
-    insertBlocks_ = (nWords + (kBlock / kWave) - 1) / (kBlock / kWave);
     while ((1ll << nbits_) < nSlots) ++nbits_;
 
     KgmtDev& d = d_;
     d.M = M;
     d.nSlots = nSlots;
     d.nWords = nWords;
+    d.nBlocks = slotsPadded_ / kBlock;
+    d.batchRule = p.batchRule;
     d.numIterations = p.numIterations;
     d.numDisc = p.numDisc;
     d.N = p.N;
@@ -78,6 +84,11 @@ KgmtPlanner::KgmtPlanner(const sbmp_kgmt_params& p, int nranks, int rank, Exchan
     d.width = p.width;
     d.height = p.height;
     d.agentLength = p.agentLength;
+    {   // exact reciprocal only for powers of two (then v * (1/L) == v / L bitwise)
+        int e = 0;
+        const float m = std::frexp(p.agentLength, &e);
+        d.invAgentLength = (m == 0.5f) ? 1.0f / p.agentLength : 0.0f;
+    }
     d.goalThreshold = p.goalThreshold;
     d.R1Size = p.width / (float)p.N;          // KGMT.cu:13
     d.R2Size = p.width / (float)(p.n * p.N);  // KGMT.cu:14
@@ -90,7 +101,8 @@ KgmtPlanner::KgmtPlanner(const sbmp_kgmt_params& p, int nranks, int rank, Exchan
     d.rngA = alloc<uint4>(slotsPadded_);
     d.rngB = alloc<uint2>(slotsPadded_);
     d.gnew = alloc<unsigned long long>(nWords);
-    d.wordOffsets = alloc<int>(nWords);
+    d.blockCount = alloc<int>(round_up(d.nBlocks, 4));   // read as int4
+    d.blockOffsets = alloc<int>(d.nBlocks);
     d.R1 = alloc<int>(d.nR1);
     d.R1Avail = alloc<int>(d.nR1);
     d.R1Valid = alloc<int>(d.nR1);
@@ -98,10 +110,11 @@ KgmtPlanner::KgmtPlanner(const sbmp_kgmt_params& p, int nranks, int rank, Exchan
     d.R1Cov = alloc<int>(d.nR1);
     d.R2Avail = alloc<uint32_t>(d.nR2 / 32);
     d.R2Snap = alloc<uint32_t>(d.nR2 / 32);
+    d.R2New = alloc<uint32_t>(d.nR2 / 32);
     d.R2Valid = alloc<int>(d.nR2);
     d.R2Invalid = alloc<int>(d.nR2);
     d.R1Score = alloc<float>(2 * d.nR1);
-    d.delta = alloc<int>(4 * d.nR1 + d.nR2);
+    d.delta = alloc<int>(4 * d.nR1);
     d.ctrl = alloc<IterCtrl>(p.numIterations + 2);
     d.status = alloc<PlannerStatus>(1);
     jumps_ = alloc<uint32_t>((size_t)nbits_ * 800);
@@ -137,7 +150,9 @@ void KgmtPlanner::begin(const float* initial, const float* goal, const float* d_
     SBMP_HIP(hipMemsetAsync(d.treeCtrl, 0, sizeof(float4) * d.M, s));
     launch_fill_i32(d.treeParent, -1, d.M, s);
     SBMP_HIP(hipMemsetAsync(d.gnew, 0, sizeof(unsigned long long) * d.nWords, s));
-    SBMP_HIP(hipMemsetAsync(d.wordOffsets, 0, sizeof(int) * d.nWords, s));
+    SBMP_HIP(hipMemsetAsync(d.blockCount, 0, sizeof(int) * round_up(d.nBlocks, 4), s));
+    SBMP_HIP(hipMemsetAsync(d.blockOffsets, 0, sizeof(int) * d.nBlocks, s));
+    SBMP_HIP(hipMemsetAsync(d.R2New, 0, sizeof(uint32_t) * (d.nR2 / 32), s));
     for (int* a : {d.R1, d.R1Avail, d.R1Valid, d.R1Invalid, d.R1Cov})
         SBMP_HIP(hipMemsetAsync(a, 0, sizeof(int) * d.nR1, s));
     SBMP_HIP(hipMemsetAsync(d.R2Avail, 0, sizeof(uint32_t) * (d.nR2 / 32), s));
@@ -145,7 +160,7 @@ void KgmtPlanner::begin(const float* initial, const float* goal, const float* d_
     SBMP_HIP(hipMemsetAsync(d.R2Valid, 0, sizeof(int) * d.nR2, s));
     SBMP_HIP(hipMemsetAsync(d.R2Invalid, 0, sizeof(int) * d.nR2, s));
     launch_fill_f32(d.R1Score, 1.0f, 2 * d.nR1, s);
-    SBMP_HIP(hipMemsetAsync(d.delta, 0, sizeof(int) * (4 * d.nR1 + d.nR2), s));
+    SBMP_HIP(hipMemsetAsync(d.delta, 0, sizeof(int) * (4 * d.nR1), s));
     SBMP_HIP(hipMemsetAsync(d.ctrl, 0, sizeof(IterCtrl) * (p_.numIterations + 2), s));
 
     // Obstacles: a private float4 copy of the caller's device array (KGMT.cu:80 takes
@@ -177,9 +192,9 @@ void KgmtPlanner::begin(const float* initial, const float* goal, const float* d_
     wallMs_ = 0.0;
     SBMP_HIP(hipStreamSynchronize(s));
     t0_ = now_ms();
-    timed_begin(K_PLAN);
-    launch_plan(d, 1, s);
-    timed_end(K_PLAN);
+    timed_begin(K_FINISH);
+    launch_finish(d, 0, 0, s);   // prepares iteration 1
+    timed_end(K_FINISH);
     SBMP_HIP(hipGetLastError());
 }
 
@@ -194,12 +209,9 @@ void KgmtPlanner::enqueue(int iterations) {
         timed_begin(K_EXPAND);
         launch_expand(d_, t, p_.agent, expandBlocks_, stream_);
         timed_end(K_EXPAND);
-        timed_begin(K_PLAN);
-        launch_plan(d_, t + 1, stream_);
-        timed_end(K_PLAN);
-        timed_begin(K_INSERT);
-        launch_insert(d_, t, insertBlocks_, stream_);
-        timed_end(K_INSERT);
+        timed_begin(K_FINISH);
+        launch_finish(d_, t, expandBlocks_, stream_);
+        timed_end(K_FINISH);
     }
     SBMP_HIP(hipGetLastError());
 }
@@ -490,7 +502,7 @@ void KgmtPlanner::collect_events() {
 
 std::vector<sbmp_kernel_stat> KgmtPlanner::kernel_stats() {
     collect_events();
-    static const char* names[K_COUNT] = {"k_expand", "k_plan", "k_insert", "k_pack", "k_merge_insert"};
+    static const char* names[K_COUNT] = {"k_expand", "k_finish", "k_pack", "k_merge_insert"};
     std::vector<sbmp_kernel_stat> out;
     for (int i = 0; i < K_COUNT; ++i) {
         sbmp_kernel_stat s;

@@ -58,12 +58,13 @@ public:
 
     std::vector<sbmp_kernel_stat> kernel_stats();
     void reset_kernel_stats();
+    void set_profiling(bool on) { p_.profileKernels = on ? 1 : 0; }
 
     // sharded pieces (kgmt_sharded.cpp)
     void enqueue_sharded_iteration(int t);
 
 private:
-    enum KernelId { K_EXPAND = 0, K_PLAN, K_INSERT, K_PACK, K_MERGE, K_COUNT };
+    enum KernelId { K_EXPAND = 0, K_FINISH, K_PACK, K_MERGE, K_COUNT };
     void timed_begin(int id);
     void timed_end(int id);
     void collect_events();
@@ -78,7 +79,7 @@ private:
     Exchange* ex_ = nullptr;
     int t_next_ = 1;
     bool begun_ = false;
-    int slotsPadded_ = 0, expandBlocks_ = 0, insertBlocks_ = 0, nbits_ = 1;
+    int slotsPadded_ = 0, expandBlocks_ = 0, nbits_ = 1;
     uint32_t* jumps_ = nullptr;
     float4* obs_ = nullptr;
     int obsCap_ = 0;

@@ -293,6 +293,13 @@ sbmp_status sbmp_kgmt_reset_kernel_stats(sbmp_kgmt* h) {
     });
 }
 
+sbmp_status sbmp_kgmt_set_profiling(sbmp_kgmt* h, int enabled) {
+    return guarded([&] {
+        PLANNER(h);
+        P.set_profiling(enabled != 0);
+    });
+}
+
 // readObstaclesFromCSV (reference src/helper/helper.cu:11-34): values separated
 // by whitespace or single commas, read line by line with operator>>.
 sbmp_status sbmp_read_obstacles_csv(const char* path, int workspaceDim, float* out, int capacity,

@@ -21,6 +21,7 @@ import numpy as np
 from . import _native as nat
 
 AGENTS = {"car": nat.SBMP_AGENT_CAR, "point": nat.SBMP_AGENT_POINT}
+BATCH_RULES = {"reference": nat.SBMP_BATCH_REFERENCE, "fill": nat.SBMP_BATCH_FILL}
 
 
 def reference_seed_from_time(t: Optional[float] = None) -> int:
@@ -96,7 +97,7 @@ class KGMT:
     def __init__(self, width: float, height: float, N: int, n: int, numIterations: int, maxTreeSize: int,
                  numDisc: int, agentLength: float, goalThreshold: float, *, samplesPerIteration: int = 0,
                  agent: str = "car", fixGNewClear: bool = False, device: int = 0, profileKernels: bool = False,
-                 _sharded=None):
+                 batchRule: str = "reference", _sharded=None):
         p = nat.KgmtParams()
         nat.call("sbmp_kgmt_default_params", ctypes.byref(p))
         p.width, p.height, p.N, p.n = width, height, N, n
@@ -107,6 +108,7 @@ class KGMT:
         p.fixGNewClear = int(bool(fixGNewClear))
         p.device = device
         p.profileKernels = int(bool(profileKernels))
+        p.batchRule = BATCH_RULES[batchRule]
         self._params = p
         h = ctypes.c_void_p()
         if _sharded is None:
@@ -263,3 +265,6 @@ class KGMT:
 
     def reset_kernel_stats(self) -> None:
         nat.call("sbmp_kgmt_reset_kernel_stats", self._h)
+
+    def set_profiling(self, enabled: bool) -> None:
+        nat.call("sbmp_kgmt_set_profiling", self._h, int(bool(enabled)))

@@ -60,7 +60,16 @@ typedef struct sbmp_kgmt_params {
     int fixGNewClear;         /* 0 = reproduce the reference's partial GNew clear */
     int device;               /* HIP device ordinal */
     int profileKernels;       /* 1 = time every kernel launch with HIP events (sbmp_kgmt_kernel_stats) */
+    int batchRule;            /* SBMP_BATCH_REFERENCE or SBMP_BATCH_FILL (needs samplesPerIteration > 0) */
 } sbmp_kgmt_params;
+
+/* Children per frontier node.  REFERENCE: 32, or floor(remaining/|G|) once 32|G|
+ * exceeds the remaining capacity (KGMT.cu:151-158), with remaining additionally
+ * capped at samplesPerIteration when that is > 0.  FILL (build extension D14):
+ * floor(samplesPerIteration/|G|) children per frontier node, so every iteration
+ * generates (almost exactly) samplesPerIteration children. */
+#define SBMP_BATCH_REFERENCE 0
+#define SBMP_BATCH_FILL 1
 
 /* Outcome of a plan (the reference's public fields treeSize_/costToGoal_, KGMT.cuh:37,40,
  * plus what its prints report, KGMT.cu:295-296). */
@@ -139,6 +148,8 @@ sbmp_status sbmp_kgmt_export_csv(sbmp_kgmt* h, const char* dir);
 
 sbmp_status sbmp_kgmt_kernel_stats(sbmp_kgmt* h, sbmp_kernel_stat* out, int capacity, int* count);
 sbmp_status sbmp_kgmt_reset_kernel_stats(sbmp_kgmt* h);
+/* Turn per-launch HIP-event timing on/off for subsequently enqueued iterations. */
+sbmp_status sbmp_kgmt_set_profiling(sbmp_kgmt* h, int enabled);
 
 /* readObstaclesFromCSV (reference src/helper/helper.cu:11-34): whitespace or
  * comma separated floats, numObstacles = floats / (2*workspaceDim).  Returns

@@ -340,7 +340,18 @@ public:
             const long long cap = p_.samplesPerIteration;
             long long remaining = (long long)M_ - treeSize_;
             if (cap > 0) remaining = std::min(remaining, cap);
-            if (32ll * nG <= remaining) {
+            if (cap > 0 && p_.batchRule == 1) {
+                // D14 (build extension): fill the batch -- every frontier node gets
+                // floor(remaining/|G|) children; more frontier than budget: one child
+                // each for the first `remaining` nodes.
+                if (nG <= remaining) {
+                    k = (int)(remaining / nG);
+                    nExp = nG;
+                } else {
+                    k = 1;
+                    nExp = (int)remaining;
+                }
+            } else if (32ll * nG <= remaining) {
                 k = 32;
                 nExp = nG;
             } else {
@@ -516,6 +527,7 @@ extern "C" {
 
 void* oracle_create(const oracle_params* p) {
     if (!p || p->N * p->N != 256 || p->n <= 0 || p->maxTreeSize <= 0 || p->numDisc <= 0) return nullptr;
+    if (p->batchRule == 1 && p->samplesPerIteration <= 0) return nullptr;
     if (p->nranks > 1 && (p->rank < 0 || p->rank >= p->nranks)) return nullptr;
     return new Oracle(*p);
 }

@@ -28,6 +28,7 @@ typedef struct oracle_params {
     int fixGNewClear;           /* 0 = reproduce the partial GNew clear (D6) */
     int threads;                /* OpenMP threads for the expansion loop (<=0: 1) */
     int nranks, rank;           /* slot-ownership sharding (1, 0 = unsharded) */
+    int batchRule;              /* 0 = reference rule + cap, 1 = fill the cap (D14) */
 } oracle_params;
 
 /* One accepted child as exchanged between ranks: slot id, 7 sample floats, parent. */

@@ -27,7 +27,7 @@ class OracleParams(ctypes.Structure):
         ("agentLength", ctypes.c_float), ("goalThreshold", ctypes.c_float),
         ("samplesPerIteration", ctypes.c_int), ("agent", ctypes.c_int),
         ("fixGNewClear", ctypes.c_int), ("threads", ctypes.c_int),
-        ("nranks", ctypes.c_int), ("rank", ctypes.c_int),
+        ("nranks", ctypes.c_int), ("rank", ctypes.c_int), ("batchRule", ctypes.c_int),
     ]
 
 
@@ -111,6 +111,7 @@ class PlannerConfig:
     samplesPerIteration: int = 0
     agent: int = 0
     fixGNewClear: int = 0
+    batchRule: int = 0
 
 
 class Oracle:
@@ -120,7 +121,7 @@ class Oracle:
         self.cfg = cfg
         p = OracleParams(cfg.width, cfg.height, cfg.N, cfg.n, cfg.numIterations, cfg.maxTreeSize,
                          cfg.numDisc, cfg.agentLength, cfg.goalThreshold, cfg.samplesPerIteration,
-                         cfg.agent, cfg.fixGNewClear, threads, nranks, rank)
+                         cfg.agent, cfg.fixGNewClear, threads, nranks, rank, cfg.batchRule)
         self._h = lib().oracle_create(ctypes.byref(p))
         if not self._h:
             raise ValueError("oracle_create rejected the parameters")
@@ -234,7 +235,7 @@ def replay(cfg: PlannerConfig, obstacles, parents: np.ndarray, controls: np.ndar
     """Invariant I1: re-propagate parents (n,4) with controls (n,3) -> (states (n,4), valid (n,))."""
     p = OracleParams(cfg.width, cfg.height, cfg.N, cfg.n, cfg.numIterations, cfg.maxTreeSize, cfg.numDisc,
                      cfg.agentLength, cfg.goalThreshold, cfg.samplesPerIteration, cfg.agent, cfg.fixGNewClear,
-                     threads, 1, 0)
+                     threads, 1, 0, cfg.batchRule)
     obs = np.ascontiguousarray(obstacles, dtype=np.float32).ravel()
     parents = np.ascontiguousarray(parents, dtype=np.float32)
     controls = np.ascontiguousarray(controls, dtype=np.float32)
