@@ -26,7 +26,8 @@ namespace sbmp {
 constexpr int kBlock = 256;          // threads per expand block = slots per ownership block
 constexpr int kWave = 64;
 constexpr int kNoGoal = 0x7fffffff;
-constexpr int kMaxR1 = 256;          // N must be 16 (reference KGMT.cu:8,501,520)
+constexpr int kN = 16;               // R1 grid side: N must be 16 (reference KGMT.cu:8,501,520)
+constexpr int kMaxR1 = kN * kN;
 constexpr int kMaxR2Words = 2048;    // n <= 16: 256*16*16 cells / 32
 
 // Per-iteration control block, written once by the plan kernel of that iteration.
@@ -134,21 +135,38 @@ SBMP_HD float xorwow_uniform(Xorwow& s) {
 // ---------------------------------------------------------------- collision
 // reference collisionCheck.cu:6-28: a segment AABB is free of an obstacle box
 // iff separated on some axis; the motion is valid iff free of every box.
-// OBS_LDS: the list is staged in LDS and every box is tested without early
+// OBS > 0: the list is staged in LDS and every box is tested without early
 // exit (independent broadcast reads, no load->compare->branch chain; the result
 // is an order-independent OR, so identical to the reference's early return).
 // Otherwise the list is read from global memory with the reference's early exit.
-template <bool OBS_LDS>
+__device__ __forceinline__ int box_overlap(float minx, float miny, float maxx, float maxy, float4 o) {
+    // (xmin, ymin, xmax, ymax).  !(a <= b), not (a > b): identical to the reference's
+    // predicate for NaN too.  Bitwise, not short-circuit: one 16-B read, four compares.
+    return (int)!(maxx <= o.x) & (int)!(o.z <= minx) & (int)!(maxy <= o.y) & (int)!(o.w <= miny);
+}
+
+// OBS: 0 = global list, reference early exit; 1 = LDS list, rolled loop;
+//      2 = LDS list, 4-way unrolled (reads batched, more VGPRs).
+template <int OBS>
 __device__ __forceinline__ bool motion_valid(float minx, float miny, float maxx, float maxy,
                                              const float4* __restrict__ obs, int nObs) {
-    if (OBS_LDS) {
-        bool hit = false;
-#pragma unroll 4
-        for (int i = 0; i < nObs; ++i) {
-            const float4 o = obs[i];   // (xmin, ymin, xmax, ymax)
-            hit |= !((maxx <= o.x) || (o.z <= minx) || (maxy <= o.y) || (o.w <= miny));
+    if (OBS == 1) {
+        int hit = 0;
+#pragma unroll 1
+        for (int i = 0; i < nObs; ++i) hit |= box_overlap(minx, miny, maxx, maxy, obs[i]);
+        return hit == 0;
+    }
+    if (OBS == 2) {
+        int hit = 0;
+        int i = 0;
+        for (; i + 4 <= nObs; i += 4) {
+            const float4 a = obs[i], b = obs[i + 1], c = obs[i + 2], e = obs[i + 3];
+            hit |= box_overlap(minx, miny, maxx, maxy, a) | box_overlap(minx, miny, maxx, maxy, b) |
+                   box_overlap(minx, miny, maxx, maxy, c) | box_overlap(minx, miny, maxx, maxy, e);
         }
-        return !hit;
+#pragma unroll 1
+        for (; i < nObs; ++i) hit |= box_overlap(minx, miny, maxx, maxy, obs[i]);
+        return hit == 0;
     }
     for (int i = 0; i < nObs; ++i) {
         const float4 o = obs[i];
@@ -168,7 +186,7 @@ struct ChildOut {
 // v / agentLength: when agentLength is a power of two, v * (1/agentLength) is the
 // same correctly rounded value (both are the exact product scaled by 2^-k), so the
 // host passes invAgentLength != 0 and the per-step division disappears.
-template <bool OBS_LDS>
+template <int OBS>
 __device__ __forceinline__ bool propagate_car(float4 p, Xorwow& rs, const KgmtDev& d, const float4* obs,
                                               ChildOut& out) {
     const float a = __builtin_fmaf(xorwow_uniform(rs), 10.0f, -5.0f);
@@ -194,7 +212,7 @@ __device__ __forceinline__ bool propagate_car(float4 p, Xorwow& rs, const KgmtDe
         v = __builtin_fmaf(a, dt, v);
         const float minx = (px > x) ? x : px, maxx = (px > x) ? px : x;
         const float miny = (py > y) ? y : py, maxy = (py > y) ? py : y;
-        if (!motion_valid<OBS_LDS>(minx, miny, maxx, maxy, obs, d.nObs)) {
+        if (!motion_valid<OBS>(minx, miny, maxx, maxy, obs, d.nObs)) {
             valid = false;
             break;
         }
@@ -207,7 +225,7 @@ __device__ __forceinline__ bool propagate_car(float4 p, Xorwow& rs, const KgmtDe
 }
 
 // Holonomic R2 point (build extension).
-template <bool OBS_LDS>
+template <int OBS>
 __device__ __forceinline__ bool propagate_point(float4 p, Xorwow& rs, const KgmtDev& d, const float4* obs,
                                                 ChildOut& out) {
     const float vx = __builtin_fmaf(xorwow_uniform(rs), 2.0f, -1.0f);
@@ -226,7 +244,7 @@ __device__ __forceinline__ bool propagate_point(float4 p, Xorwow& rs, const Kgmt
         }
         const float minx = (px > x) ? x : px, maxx = (px > x) ? px : x;
         const float miny = (py > y) ? y : py, maxy = (py > y) ? py : y;
-        if (!motion_valid<OBS_LDS>(minx, miny, maxx, maxy, obs, d.nObs)) {
+        if (!motion_valid<OBS>(minx, miny, maxx, maxy, obs, d.nObs)) {
             valid = false;
             break;
         }

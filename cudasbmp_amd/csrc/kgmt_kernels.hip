@@ -18,6 +18,7 @@
 // expanded each iteration and new rows are appended contiguously, so G is
 // always the row range [gLo, treeSize) (parity-tested against the oracle,
 // which keeps the literal boolean scans).
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
 #include "kgmt_device.h"
@@ -29,9 +30,19 @@
 
 namespace sbmp {
 
-// ------------------------------------------------------------------ expand
-
 // ------------------------------------------------------------------ helpers
+// a / b for 0 <= a < 2^24, 1 <= b: float estimate (relative error < 2^-21, so
+// off by at most 1 for a < 2^24) + exact integer correction of up to 2 steps.
+__device__ __forceinline__ int div_small(int a, int b) {
+    int q = (int)((float)a * __builtin_amdgcn_rcpf((float)b));
+    int r = a - q * b;
+    if (r < 0) { --q; r += b; }
+    if (r < 0) { --q; r += b; }
+    if (r >= b) { ++q; r -= b; }
+    if (r >= b) { ++q; }
+    return q;
+}
+
 __device__ __forceinline__ int wave_sum(int v) {
 #pragma unroll
     for (int off = kWave / 2; off > 0; off >>= 1) v += __shfl_xor(v, off, kWave);
@@ -62,46 +73,66 @@ __device__ __forceinline__ void block_prefix_total(const int* __restrict__ count
 }
 
 // ------------------------------------------------------------------ expand
-// One thread per child slot; one 256-thread block per 256-slot ownership block.
+// One thread per child slot.  A workgroup of 256 threads processes CH ownership
+// blocks of 256 slots each (CH chunks): the XORWOW states of all its chunks are
+// loaded up front, so the stores of chunk c drain while chunk c+1 computes.
 // Outputs: child state/controls/parent (2 x 16 B), XORWOW state (16 + 8 B),
-// GNew bits (one 8-B word per wave), the block's GNew popcount, block-private
-// R1 counters flushed once per block, R2 valid/invalid counters aggregated per
-// (cell, validity) in an LDS hash table and flushed once per distinct key, and
-// R2New bits for cells that were unavailable in the iteration-start snapshot.
-constexpr int kHash = 512;
-
-template <int AGENT, bool OBS_LDS>
+// GNew bits (one 8-B word per wave and chunk), the GNew popcount of each
+// 256-slot block, workgroup-private R1 counters flushed once, R2 valid/invalid
+// counters aggregated per (cell, validity) in an LDS hash table and flushed once
+// per distinct key, and R2New bits for cells unavailable in the snapshot.
+template <int AGENT, int OBS, int CH>
 __global__ __launch_bounds__(kBlock) void k_expand(KgmtDev d, int t) {
+    constexpr int kHash = 512 * CH;
     extern __shared__ float4 sObs[];
     __shared__ float sScore[kMaxR1];
-    __shared__ int sCnt[4][kMaxR1];   // R1, R1Valid, R1Invalid, R1AvailSet (block-private)
+    __shared__ int sCnt[4][kMaxR1];   // R1, R1Valid, R1Invalid, R1AvailSet (workgroup-private)
     __shared__ int sKey[kHash];       // (r2 << 1 | valid) -> count
     __shared__ int sVal[kHash];
-    __shared__ int sWaveCnt[kBlock / kWave];
+    __shared__ int sWaveCnt[CH][kBlock / kWave];
+
+    const int tid = threadIdx.x;
+    const int lane = tid & (kWave - 1);
+    const int wave = tid >> 6;
+    int gblock[CH], slot[CH];
+#pragma unroll
+    for (int ch = 0; ch < CH; ++ch) {
+        gblock[ch] = d.rank + d.nranks * ((int)blockIdx.x * CH + ch);   // block-cyclic slot ownership
+        slot[ch] = gblock[ch] * kBlock + tid;
+    }
+
+    // Latency: issue every load that does not depend on the control block before
+    // waiting for it (slot arrays are allocated to a whole number of workgroups; the
+    // score buffer of iteration t is t & 1).  Only the parent-row loads wait on ctrl.
+    uint4 ra[CH];
+    uint2 rb[CH];
+    unsigned long long oldWord[CH];
+#pragma unroll
+    for (int ch = 0; ch < CH; ++ch) {
+        ra[ch] = d.rngA[slot[ch]];
+        rb[ch] = d.rngB[slot[ch]];
+        oldWord[ch] = (lane == 0) ? d.gnew[slot[ch] >> 6] : 0ull;
+    }
+    const float scoreReg = (tid < d.nR1) ? d.R1Score[(t & 1) * d.nR1 + tid] : 0.0f;
+    const float4 obsReg = (OBS > 0 && tid < d.nObs) ? d.obstacles[tid] : make_float4(0.f, 0.f, 0.f, 0.f);
 
     const IterCtrl c = d.ctrl[t];
     if (!c.run || d.status->goalIdx != kNoGoal) return;   // grid-uniform
     if (blockIdx.x == 0 && threadIdx.x == 0) d.ctrl[t].executed = 1;
-    const int gblock = d.rank + d.nranks * (int)blockIdx.x;  // block-cyclic slot ownership
-    const int slotBase = gblock * kBlock;
-    const int tid = threadIdx.x;
-    const int lane = tid & (kWave - 1);
-    const int wave = tid >> 6;
+    if (gblock[0] * kBlock >= c.H) return;   // past every batch and every stale bit (workgroup-uniform)
 
-    if (slotBase >= c.S) {
-        // Past this iteration's batch: publish the stale GNew bits' count (D6) so the
-        // compaction sees them; nothing else to do.
-        if (slotBase < c.H) {
-            if (lane == 0) sWaveCnt[wave] = __popcll(d.gnew[(slotBase >> 6) + wave]);
-            __syncthreads();
-            if (tid == 0) d.blockCount[gblock] = sWaveCnt[0] + sWaveCnt[1] + sWaveCnt[2] + sWaveCnt[3];
-        }
-        return;
+    float4 p[CH];
+    int parent[CH];
+#pragma unroll
+    for (int ch = 0; ch < CH; ++ch) {
+        const bool act = slot[ch] < c.S;
+        const int g = !act ? 0 : (c.k == 32) ? (slot[ch] >> 5) : div_small(slot[ch], c.k);   // slot = g*k + i
+        parent[ch] = c.gLo + g;
+        p[ch] = act ? d.treeState[parent[ch]] : make_float4(0.f, 0.f, 0.f, 0.f);
     }
 
-    const float* score = d.R1Score + c.scoreBuf * d.nR1;
+    if (tid < d.nR1) sScore[tid] = scoreReg;
     for (int i = tid; i < d.nR1; i += kBlock) {
-        sScore[i] = score[i];
         sCnt[0][i] = 0;
         sCnt[1][i] = 0;
         sCnt[2][i] = 0;
@@ -111,70 +142,68 @@ __global__ __launch_bounds__(kBlock) void k_expand(KgmtDev d, int t) {
         sKey[i] = -1;
         sVal[i] = 0;
     }
-    if (OBS_LDS)
-        for (int i = tid; i < d.nObs; i += kBlock) sObs[i] = d.obstacles[i];
+    if (OBS > 0) {
+        if (tid < d.nObs) sObs[tid] = obsReg;
+        for (int i = tid + kBlock; i < d.nObs; i += kBlock) sObs[i] = d.obstacles[i];
+    }
     __syncthreads();
-    const float4* obs = OBS_LDS ? sObs : d.obstacles;
+    const float4* obs = (OBS > 0) ? sObs : d.obstacles;
 
-    const int slot = slotBase + tid;
-    bool accept = false;
-    if (slot < c.S) {
-        const int g = (c.k == 32) ? (slot >> 5) : (slot / c.k);   // slot = g*k + i
-        const int parent = c.gLo + g;
-        const float4 p = d.treeState[parent];
-        const uint4 ra = d.rngA[slot];
-        const uint2 rb = d.rngB[slot];
-        Xorwow rs{ra.x, ra.y, ra.z, ra.w, rb.x, rb.y};
-        ChildOut ch;
-        const bool valid = (AGENT == 0) ? propagate_car<OBS_LDS>(p, rs, d, obs, ch)
-                                        : propagate_point<OBS_LDS>(p, rs, d, obs, ch);
-        const int r1 = getR1(ch.state.x, ch.state.y, d.R1Size, d.N);
-        const int r2 = getR2(ch.state.x, ch.state.y, r1, d.R1Size, d.N, d.R2Size, d.n);
-        if (valid) {
-            const float u = xorwow_uniform(rs);   // KGMT.cu:395
-            if (r1 >= 0 && r2 >= 0) {
-                const bool r2Avail = (d.R2Snap[r2 >> 5] >> (r2 & 31)) & 1u;
-                accept = (u <= sScore[r1]) || !r2Avail;
-            }
-        }
-        // Region counters (KGMT.cu:392-411; D3: in-grid cells only).
-        if (r1 >= 0) {
-            atomicAdd(&sCnt[0][r1], 1);
+#pragma unroll
+    for (int ch = 0; ch < CH; ++ch) {
+        bool accept = false;
+        if (slot[ch] < c.S) {
+            Xorwow rs{ra[ch].x, ra[ch].y, ra[ch].z, ra[ch].w, rb[ch].x, rb[ch].y};
+            ChildOut out;
+            const bool valid = (AGENT == 0) ? propagate_car<OBS>(p[ch], rs, d, obs, out)
+                                            : propagate_point<OBS>(p[ch], rs, d, obs, out);
+            const int r1 = getR1(out.state.x, out.state.y, d.R1Size, kN);   // N = 16 (KGMT.cu:8)
+            const int r2 = getR2(out.state.x, out.state.y, r1, d.R1Size, kN, d.R2Size, d.n);
             if (valid) {
-                atomicAdd(&sCnt[1][r1], 1);
-                sCnt[3][r1] = 1;
-            } else {
-                atomicAdd(&sCnt[2][r1], 1);
-            }
-        }
-        if (r2 >= 0) {
-            const int key = (r2 << 1) | (valid ? 1 : 0);
-            uint32_t h = ((uint32_t)key * 2654435761u) >> 23;   // 9 bits
-            while (true) {
-                const int old = atomicCAS(&sKey[h], -1, key);
-                if (old == -1 || old == key) {
-                    atomicAdd(&sVal[h], 1);
-                    break;
+                const float u = xorwow_uniform(rs);   // KGMT.cu:395
+                if (r1 >= 0 && r2 >= 0) {
+                    const bool r2Avail = (d.R2Snap[r2 >> 5] >> (r2 & 31)) & 1u;
+                    accept = (u <= sScore[r1]) || !r2Avail;
                 }
-                h = (h + 1) & (kHash - 1);
             }
+            // Region counters (KGMT.cu:392-411; D3: in-grid cells only).
+            if (r1 >= 0) {
+                atomicAdd(&sCnt[0][r1], 1);
+                if (valid) {
+                    atomicAdd(&sCnt[1][r1], 1);
+                    sCnt[3][r1] = 1;
+                } else {
+                    atomicAdd(&sCnt[2][r1], 1);
+                }
+            }
+            if (r2 >= 0) {
+                const int key = (r2 << 1) | (valid ? 1 : 0);
+                uint32_t h = ((uint32_t)key * 2654435761u) & (kHash - 1);
+                while (true) {
+                    const int old = atomicCAS(&sKey[h], -1, key);
+                    if (old == -1 || old == key) {
+                        atomicAdd(&sVal[h], 1);
+                        break;
+                    }
+                    h = (h + 1) & (kHash - 1);
+                }
+            }
+            d.uState[slot[ch]] = out.state;
+            d.uCtrl[slot[ch]] = make_float4(out.a, out.steer, out.dur, __int_as_float(parent[ch]));
+            d.rngA[slot[ch]] = make_uint4(rs.v0, rs.v1, rs.v2, rs.v3);
+            d.rngB[slot[ch]] = make_uint2(rs.v4, rs.d);
         }
-
-        d.uState[slot] = ch.state;
-        d.uCtrl[slot] = make_float4(ch.a, ch.steer, ch.dur, __int_as_float(parent));
-        d.rngA[slot] = make_uint4(rs.v0, rs.v1, rs.v2, rs.v3);
-        d.rngB[slot] = make_uint2(rs.v4, rs.d);
-    }
-    // GNew |= accept (stale bits survive, D6).  A wave covers one 64-bit word.
-    const unsigned long long mask = __ballot(accept);
-    if (lane == 0) {
-        const unsigned long long old = d.gnew[slot >> 6];
-        const unsigned long long now = old | mask;
-        if (now != old) d.gnew[slot >> 6] = now;
-        sWaveCnt[wave] = __popcll(now);
+        // GNew |= accept (stale bits survive, D6).  A wave covers one 64-bit word.
+        const unsigned long long mask = __ballot(accept);
+        if (lane == 0) {
+            const unsigned long long now = oldWord[ch] | mask;
+            if (now != oldWord[ch]) d.gnew[slot[ch] >> 6] = now;
+            sWaveCnt[ch][wave] = __popcll(now);   // chunks past S: the stale bits' count
+        }
     }
     __syncthreads();
-    if (tid == 0) d.blockCount[gblock] = sWaveCnt[0] + sWaveCnt[1] + sWaveCnt[2] + sWaveCnt[3];
+    if (tid < CH && gblock[tid] * kBlock < c.H)
+        d.blockCount[gblock[tid]] = sWaveCnt[tid][0] + sWaveCnt[tid][1] + sWaveCnt[tid][2] + sWaveCnt[tid][3];
     for (int i = tid; i < d.nR1; i += kBlock) {
         if (sCnt[0][i]) atomicAdd(&d.delta[i], sCnt[0][i]);
         if (sCnt[1][i]) atomicAdd(&d.delta[d.nR1 + i], sCnt[1][i]);
@@ -361,17 +390,20 @@ __device__ void plan_iteration(const KgmtDev& d, int t) {
 __device__ void insert_block(const KgmtDev& d, int t, int gblock) {
     __shared__ int sRed[2][kBlock / kWave];
     __shared__ int sWaveCnt[kBlock / kWave];
-    const IterCtrl c = d.ctrl[t];
-    if (!c.executed) return;
-    if (gblock * kBlock >= c.H) return;
-    if (d.blockCount[gblock] == 0) return;   // no accepted (or stale) slot: nothing to insert or clear
-    int pre, A;
-    block_prefix_total(d.blockCount, (c.H + kBlock - 1) / kBlock, gblock, &pre, &A, sRed);
-
     const int lane = threadIdx.x & (kWave - 1);
     const int wave = threadIdx.x >> 6;
     const int w = gblock * (kBlock / kWave) + wave;
+    // Loads that do not depend on the control block go first (blockCount entries at
+    // or past the high-water block were never written and are zero).
     const unsigned long long word = d.gnew[w];
+    const int myCount = d.blockCount[gblock];
+    const IterCtrl c = d.ctrl[t];
+    if (!c.executed) return;
+    if (gblock * kBlock >= c.H) return;
+    if (myCount == 0) return;   // no accepted (or stale) slot: nothing to insert or clear
+    int pre, A;
+    block_prefix_total(d.blockCount, d.nBlocks, gblock, &pre, &A, sRed);
+
     if (lane == 0) sWaveCnt[wave] = __popcll(word);
     __syncthreads();
     int waveOff = pre;
@@ -501,21 +533,46 @@ __global__ void k_export_unexplored(KgmtDev d, float* samples, int* uParent) {
 }
 
 // ------------------------------------------------------------------ launchers
-void launch_expand(const KgmtDev& d, int t, int agent, int blocks, hipStream_t s) {
-    const bool lds = d.nObs <= kMaxLdsObs;
-    const size_t shm = lds ? sizeof(float4) * (size_t)d.nObs : 0;
-    if (agent == 0) {
-        if (lds) hipLaunchKernelGGL((k_expand<0, true>), dim3(blocks), dim3(kBlock), shm, s, d, t);
-        else hipLaunchKernelGGL((k_expand<0, false>), dim3(blocks), dim3(kBlock), 0, s, d, t);
+// With timing events, hipExtLaunchKernelGGL stamps them from the kernel's own
+// dispatch packet (start/end of execution, as rocprofv3's kernel trace does);
+// events recorded as separate stream packets would add the dispatch latency.
+template <typename K, typename... Args>
+static void launch(K kernel, dim3 grid, dim3 block, size_t shm, hipStream_t s, const KernelTiming& tm,
+                   Args... args) {
+    if (tm.start)
+        hipExtLaunchKernelGGL(kernel, grid, block, (uint32_t)shm, s, tm.start, tm.stop, 0u, args...);
+    else
+        hipLaunchKernelGGL(kernel, grid, block, shm, s, args...);
+}
+
+template <int AGENT, int CH>
+static void launch_expand_agent(const KgmtDev& d, int t, int blocks, int variant, hipStream_t s,
+                                const KernelTiming& tm) {
+    const size_t shm = sizeof(float4) * (size_t)d.nObs;
+    const dim3 grid(blocks / CH);
+    if (d.nObs > kMaxLdsObs)
+        launch(k_expand<AGENT, 0, CH>, grid, dim3(kBlock), 0, s, tm, d, t);
+    else if (variant == 2)
+        launch(k_expand<AGENT, 2, CH>, grid, dim3(kBlock), shm, s, tm, d, t);
+    else
+        launch(k_expand<AGENT, 1, CH>, grid, dim3(kBlock), shm, s, tm, d, t);
+}
+
+void launch_expand(const KgmtDev& d, int t, int agent, int blocks, int variant, int chunks, hipStream_t s,
+                   const KernelTiming& tm) {
+    if (chunks == 2) {
+        if (agent == 0) launch_expand_agent<0, 2>(d, t, blocks, variant, s, tm);
+        else launch_expand_agent<1, 2>(d, t, blocks, variant, s, tm);
     } else {
-        if (lds) hipLaunchKernelGGL((k_expand<1, true>), dim3(blocks), dim3(kBlock), shm, s, d, t);
-        else hipLaunchKernelGGL((k_expand<1, false>), dim3(blocks), dim3(kBlock), 0, s, d, t);
+        if (agent == 0) launch_expand_agent<0, 1>(d, t, blocks, variant, s, tm);
+        else launch_expand_agent<1, 1>(d, t, blocks, variant, s, tm);
     }
 }
 
-void launch_finish(const KgmtDev& d, int t, int insertBlocks, hipStream_t s) {
-    hipLaunchKernelGGL(k_finish, dim3(1 + insertBlocks), dim3(kBlock), 0, s, d, t);
+void launch_finish(const KgmtDev& d, int t, int insertBlocks, hipStream_t s, const KernelTiming& tm) {
+    launch(k_finish, dim3(1 + insertBlocks), dim3(kBlock), 0, s, tm, d, t);
 }
+
 void launch_fill_i32(int* p, int v, long long n, hipStream_t s) {
     if (n <= 0) return;
     const int blocks = (int)std::min<long long>((n + 255) / 256, 4096);

@@ -10,10 +10,21 @@
 
 namespace sbmp {
 
-void launch_expand(const KgmtDev& d, int t, int agent, int blocks, hipStream_t s);
+// Optional start/stop events stamped by the kernel's dispatch packet.
+struct KernelTiming {
+    hipEvent_t start = nullptr;
+    hipEvent_t stop = nullptr;
+};
+
+// variant: obstacle-loop form for LDS-resident lists (1 = rolled, 2 = 4-way batched);
+// lists longer than kMaxLdsObs always use the global early-exit form.
+// chunks: 256-slot ownership blocks per workgroup (1 or 2; blocks % chunks == 0).
+void launch_expand(const KgmtDev& d, int t, int agent, int blocks, int variant, int chunks, hipStream_t s,
+                   const KernelTiming& tm = KernelTiming());
 // k_finish(t): insert iteration t (insertBlocks blocks) + prepare iteration t+1.
 // t = 0 prepares iteration 1 only (insertBlocks = 0).
-void launch_finish(const KgmtDev& d, int t, int insertBlocks, hipStream_t s);
+void launch_finish(const KgmtDev& d, int t, int insertBlocks, hipStream_t s,
+                   const KernelTiming& tm = KernelTiming());
 void launch_fill_i32(int* p, int v, long long n, hipStream_t s);
 void launch_fill_f32(float* p, float v, long long n, hipStream_t s);
 void launch_init_slots(const KgmtDev& d, const Xorwow& base, const uint32_t* jumps, int nbits, int blocks,

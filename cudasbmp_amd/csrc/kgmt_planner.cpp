@@ -57,10 +57,12 @@ KgmtPlanner::KgmtPlanner(const sbmp_kgmt_params& p, int nranks, int rank, Exchan
     if (p.device < 0 || p.device >= ndev) throw Error(SBMP_ERR_INVALID_ARGUMENT, "no such HIP device");
     SBMP_HIP(hipSetDevice(p.device));
     SBMP_HIP(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+    if (const char* v = getenv("SBMP_EXPAND_VARIANT")) expandVariant_ = atoi(v) == 2 ? 2 : 1;
+    if (const char* v = getenv("SBMP_EXPAND_CHUNKS")) expandChunks_ = atoi(v) == 2 ? 2 : 1;
 
     const int M = p.maxTreeSize;
     const int nSlots = p.samplesPerIteration > 0 ? std::min(M, p.samplesPerIteration) : M;
-    slotsPadded_ = round_up(nSlots, (long long)kBlock * nranks);
+    slotsPadded_ = round_up(nSlots, 2ll * kBlock * nranks);   // whole workgroups at 1 or 2 chunks
     expandBlocks_ = slotsPadded_ / kBlock / nranks;
     const int nWords = slotsPadded_ / kWave;
     while ((1ll << nbits_) < nSlots) ++nbits_;
@@ -192,9 +194,7 @@ void KgmtPlanner::begin(const float* initial, const float* goal, const float* d_
     wallMs_ = 0.0;
     SBMP_HIP(hipStreamSynchronize(s));
     t0_ = now_ms();
-    timed_begin(K_FINISH);
-    launch_finish(d, 0, 0, s);   // prepares iteration 1
-    timed_end(K_FINISH);
+    launch_finish(d, 0, 0, s, timing(K_FINISH));   // prepares iteration 1
     SBMP_HIP(hipGetLastError());
 }
 
@@ -206,12 +206,8 @@ void KgmtPlanner::enqueue(int iterations) {
             enqueue_sharded_iteration(t);
             continue;
         }
-        timed_begin(K_EXPAND);
-        launch_expand(d_, t, p_.agent, expandBlocks_, stream_);
-        timed_end(K_EXPAND);
-        timed_begin(K_FINISH);
-        launch_finish(d_, t, expandBlocks_, stream_);
-        timed_end(K_FINISH);
+        launch_expand(d_, t, p_.agent, expandBlocks_, expandVariant_, expandChunks_, stream_, timing(K_EXPAND));
+        launch_finish(d_, t, expandBlocks_, stream_, timing(K_FINISH));
     }
     SBMP_HIP(hipGetLastError());
 }
@@ -466,10 +462,12 @@ void KgmtPlanner::export_csv(const std::string& dir) {
 }
 
 // ---------------------------------------------------------------- profiling
-void KgmtPlanner::timed_begin(int id) {
-    if (!p_.profileKernels) return;
-    hipEvent_t a, b;
-    for (hipEvent_t* e : {&a, &b}) {
+// Events for one launch (null pair when profiling is off).  They are handed to
+// hipExtLaunchKernelGGL, which stamps them with the kernel's own start/end.
+KernelTiming KgmtPlanner::timing(int id) {
+    KernelTiming tm;
+    if (!p_.profileKernels) return tm;
+    for (hipEvent_t* e : {&tm.start, &tm.stop}) {
         if (!eventPool_.empty()) {
             *e = eventPool_.back();
             eventPool_.pop_back();
@@ -477,14 +475,8 @@ void KgmtPlanner::timed_begin(int id) {
             SBMP_HIP(hipEventCreate(e));
         }
     }
-    pending_.push_back({id, a, b});
-    SBMP_HIP(hipEventRecord(a, stream_));
-}
-
-void KgmtPlanner::timed_end(int id) {
-    if (!p_.profileKernels) return;
-    (void)id;
-    SBMP_HIP(hipEventRecord(pending_.back().b, stream_));
+    pending_.push_back({id, tm.start, tm.stop});
+    return tm;
 }
 
 void KgmtPlanner::collect_events() {
@@ -494,15 +486,25 @@ void KgmtPlanner::collect_events() {
         SBMP_HIP(hipEventElapsedTime(&ms, q.a, q.b));
         launches_[q.id] += 1;
         totalMs_[q.id] += ms;
+        samples_[q.id].push_back(ms);
         eventPool_.push_back(q.a);
         eventPool_.push_back(q.b);
     }
     pending_.clear();
 }
 
+static const char* kKernelNames[] = {"k_expand", "k_finish", "k_pack", "k_merge_insert"};
+
+std::vector<float> KgmtPlanner::kernel_samples(const std::string& name) {
+    collect_events();
+    for (int i = 0; i < K_COUNT; ++i)
+        if (name == kKernelNames[i]) return samples_[i];
+    throw Error(SBMP_ERR_INVALID_ARGUMENT, "unknown kernel " + name);
+}
+
 std::vector<sbmp_kernel_stat> KgmtPlanner::kernel_stats() {
     collect_events();
-    static const char* names[K_COUNT] = {"k_expand", "k_finish", "k_pack", "k_merge_insert"};
+    const char* const* names = kKernelNames;
     std::vector<sbmp_kernel_stat> out;
     for (int i = 0; i < K_COUNT; ++i) {
         sbmp_kernel_stat s;
@@ -520,6 +522,7 @@ void KgmtPlanner::reset_kernel_stats() {
     for (int i = 0; i < K_COUNT; ++i) {
         launches_[i] = 0;
         totalMs_[i] = 0.0;
+        samples_[i].clear();
     }
 }
 

@@ -8,6 +8,7 @@
 #include <vector>
 
 #include "kgmt_device.h"
+#include "kgmt_launch.h"
 #include "sbmp/sbmp.h"
 
 namespace sbmp {
@@ -59,14 +60,14 @@ public:
     std::vector<sbmp_kernel_stat> kernel_stats();
     void reset_kernel_stats();
     void set_profiling(bool on) { p_.profileKernels = on ? 1 : 0; }
+    std::vector<float> kernel_samples(const std::string& name);
 
     // sharded pieces (kgmt_sharded.cpp)
     void enqueue_sharded_iteration(int t);
 
 private:
     enum KernelId { K_EXPAND = 0, K_FINISH, K_PACK, K_MERGE, K_COUNT };
-    void timed_begin(int id);
-    void timed_end(int id);
+    KernelTiming timing(int id);
     void collect_events();
     void read_ctrl(std::vector<IterCtrl>& c, PlannerStatus& st);
     int last_executed(const std::vector<IterCtrl>& c) const;
@@ -80,6 +81,8 @@ private:
     int t_next_ = 1;
     bool begun_ = false;
     int slotsPadded_ = 0, expandBlocks_ = 0, nbits_ = 1;
+    int expandVariant_ = 1;   // SBMP_EXPAND_VARIANT (obstacle-loop form, A/B knob)
+    int expandChunks_ = 1;    // SBMP_EXPAND_CHUNKS (256-slot blocks per expand workgroup)
     uint32_t* jumps_ = nullptr;
     float4* obs_ = nullptr;
     int obsCap_ = 0;
@@ -95,6 +98,7 @@ private:
     std::vector<hipEvent_t> eventPool_;
     long long launches_[K_COUNT] = {0};
     double totalMs_[K_COUNT] = {0};
+    std::vector<float> samples_[K_COUNT];
 
     friend class ShardedDriver;
 };

@@ -293,6 +293,17 @@ sbmp_status sbmp_kgmt_reset_kernel_stats(sbmp_kgmt* h) {
     });
 }
 
+sbmp_status sbmp_kgmt_kernel_samples(sbmp_kgmt* h, const char* name, float* out, int capacity, int* count) {
+    return guarded([&] {
+        PLANNER(h);
+        REQUIRE(name, "NULL name");
+        std::vector<float> v = P.kernel_samples(name);
+        const int n = std::min<int>(capacity, (int)v.size());
+        if (out && n > 0) memcpy(out, v.data(), sizeof(float) * n);
+        if (count) *count = (int)v.size();
+    });
+}
+
 sbmp_status sbmp_kgmt_set_profiling(sbmp_kgmt* h, int enabled) {
     return guarded([&] {
         PLANNER(h);

@@ -266,5 +266,14 @@ class KGMT:
     def reset_kernel_stats(self) -> None:
         nat.call("sbmp_kgmt_reset_kernel_stats", self._h)
 
+    def kernel_samples(self, name: str) -> np.ndarray:
+        """Per-launch durations (ms) of kernel `name` since the last reset_kernel_stats()."""
+        cnt = ctypes.c_int()
+        nat.call("sbmp_kgmt_kernel_samples", self._h, name.encode(), None, 0, ctypes.byref(cnt))
+        out = np.zeros(max(1, cnt.value), dtype=np.float32)
+        nat.call("sbmp_kgmt_kernel_samples", self._h, name.encode(), out.ctypes.data_as(ctypes.c_void_p),
+                 cnt.value, ctypes.byref(cnt))
+        return out[: cnt.value]
+
     def set_profiling(self, enabled: bool) -> None:
         nat.call("sbmp_kgmt_set_profiling", self._h, int(bool(enabled)))

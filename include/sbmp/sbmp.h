@@ -150,6 +150,8 @@ sbmp_status sbmp_kgmt_kernel_stats(sbmp_kgmt* h, sbmp_kernel_stat* out, int capa
 sbmp_status sbmp_kgmt_reset_kernel_stats(sbmp_kgmt* h);
 /* Turn per-launch HIP-event timing on/off for subsequently enqueued iterations. */
 sbmp_status sbmp_kgmt_set_profiling(sbmp_kgmt* h, int enabled);
+/* Individual launch durations (ms, launch order) of kernel `name` since the last reset. */
+sbmp_status sbmp_kgmt_kernel_samples(sbmp_kgmt* h, const char* name, float* out, int capacity, int* count);
 
 /* readObstaclesFromCSV (reference src/helper/helper.cu:11-34): whitespace or
  * comma separated floats, numObstacles = floats / (2*workspaceDim).  Returns

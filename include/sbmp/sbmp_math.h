@@ -160,12 +160,14 @@ SBMP_HD void sincosf_d(float x, float* s, float* c) {
     const float r = reduce_pio2(x, &q);
     const float sp = sin_poly(r);
     const float cp = cos_poly(r);
-    switch (q & 3) {
-        case 0: *s = sp;  *c = cp;  break;
-        case 1: *s = cp;  *c = -sp; break;
-        case 2: *s = -sp; *c = -cp; break;
-        default: *s = -cp; *c = sp; break;
-    }
+    // Quadrant q mod 4: (s, c) = (sp, cp), (cp, -sp), (-sp, -cp), (-cp, sp).
+    // Branch-free: swap on odd q, then exact sign flips (bit 1 of q for s,
+    // bit 1 of q+1 for c).
+    const bool odd = (q & 1) != 0;
+    const float s0 = odd ? cp : sp;
+    const float c0 = odd ? sp : cp;
+    *s = u2f(f2u(s0) ^ ((uint32_t)(q & 2) << 30));
+    *c = u2f(f2u(c0) ^ ((uint32_t)((q + 1) & 2) << 30));
 }
 
 SBMP_HD float sinf_d(float x) {

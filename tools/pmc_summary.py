@@ -1,0 +1,74 @@
+"""Summarise rocprofv3 --pmc CSVs (tools/profile_pmc.sh) per kernel.
+
+    python tools/pmc_summary.py gpurun_out/pmc [--json profiles/pmc_traffic.json]
+
+Per kernel: mean of every counter over its steady-state dispatches (the first
+`--skip` dispatches of each kernel are warm-up).  HBM traffic per launch uses the
+gfx950 correction from MI355X_MICROARCH.md §HBM: FETCH_SIZE reads half the bytes
+of wide coalesced streams, so fetched bytes = 2 * FETCH_SIZE KiB; WRITE_SIZE is
+exact for 16-B-per-lane stores.
+"""
+import argparse
+import csv
+import glob
+import json
+import os
+from collections import defaultdict
+
+import numpy as np
+
+
+def load(dirpath):
+    per = defaultdict(lambda: defaultdict(list))   # kernel -> counter -> [values by dispatch]
+    for f in glob.glob(os.path.join(dirpath, "**", "*counter_collection.csv"), recursive=True):
+        rows = list(csv.DictReader(open(f)))
+        by_disp = defaultdict(dict)
+        names = {}
+        for r in rows:
+            d = int(r["Dispatch_Id"])
+            by_disp[d][r["Counter_Name"]] = by_disp[d].get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
+            names[d] = r["Kernel_Name"]
+        for d in sorted(by_disp):
+            for k, v in by_disp[d].items():
+                per[names[d]][k].append(v)
+    return per
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("dir")
+    ap.add_argument("--skip", type=int, default=25)
+    ap.add_argument("--json", default=None)
+    ap.add_argument("--samples-per-launch", type=float, default=None,
+                    help="children per k_expand launch in the profiled run (for bytes/child)")
+    a = ap.parse_args()
+    summary = {}
+    for sub in ("sq", "sq2", "fetch", "write"):
+        for kern, ctrs in load(os.path.join(a.dir, sub)).items():
+            short = kern.split("(")[0].replace("void ", "").replace("sbmp::", "")
+            for c, vals in ctrs.items():
+                v = np.array(vals[a.skip:] if len(vals) > a.skip + 3 else vals)
+                summary.setdefault(short, {})[c] = float(np.median(v))
+    for k, cs in summary.items():
+        print(k)
+        for c, v in sorted(cs.items()):
+            print(f"   {c:24s} {v:16.1f}")
+    if a.json:
+        out = {}
+        for k, cs in summary.items():
+            if "FETCH_SIZE" in cs and "WRITE_SIZE" in cs:
+                rd = 2.0 * cs["FETCH_SIZE"] * 1024.0
+                wr = cs["WRITE_SIZE"] * 1024.0
+                key = "k_expand" if k.startswith("k_expand") else k
+                out[key] = {"kernel": k, "fetch_size_kib": cs["FETCH_SIZE"], "write_size_kib": cs["WRITE_SIZE"],
+                            "hbm_read_bytes": rd, "hbm_write_bytes": wr, "hbm_bytes_per_launch": rd + wr,
+                            "correction": "read = 2 x FETCH_SIZE (gfx950, MI355X_MICROARCH.md HBM)"}
+                if key == "k_expand" and a.samples_per_launch:
+                    out[key]["hbm_bytes_per_child"] = (rd + wr) / a.samples_per_launch
+        with open(a.json, "w") as f:
+            json.dump(out, f, indent=1)
+        print("wrote", a.json)
+
+
+if __name__ == "__main__":
+    main()
