@@ -66,7 +66,8 @@ EXPORTED_SYMBOLS = (
     "sbmp_kgmt_enqueue", "sbmp_kgmt_sync", "sbmp_kgmt_result", "sbmp_kgmt_stream", "sbmp_kgmt_copy_tree",
     "sbmp_kgmt_copy_unexplored", "sbmp_kgmt_copy_flags", "sbmp_kgmt_copy_regions", "sbmp_kgmt_num_slots",
     "sbmp_kgmt_copy_rng", "sbmp_kgmt_iter_log", "sbmp_kgmt_export_csv", "sbmp_kgmt_kernel_stats",
-    "sbmp_kgmt_reset_kernel_stats", "sbmp_kgmt_set_profiling", "sbmp_kgmt_kernel_samples", "sbmp_read_obstacles_csv", "sbmp_device_upload_f32", "sbmp_device_free",
+    "sbmp_kgmt_reset_kernel_stats", "sbmp_kgmt_set_profiling", "sbmp_kgmt_kernel_samples", "sbmp_kgmt_enqueue_delay",
+    "sbmp_read_obstacles_csv", "sbmp_device_upload_f32", "sbmp_device_free",
     "sbmp_device_count", "sbmp_comm_get_unique_id", "sbmp_kgmt_create_sharded",
 )
 
@@ -116,6 +117,7 @@ def lib():
         "sbmp_kgmt_reset_kernel_stats": [vp],
         "sbmp_kgmt_set_profiling": [vp, i],
         "sbmp_kgmt_kernel_samples": [vp, ctypes.c_char_p, vp, i, P(i)],
+        "sbmp_kgmt_enqueue_delay": [vp, ctypes.c_double],
         "sbmp_read_obstacles_csv": [ctypes.c_char_p, i, vp, i, P(i)],
         "sbmp_device_upload_f32": [vp, ctypes.c_size_t, P(vp)],
         "sbmp_device_free": [vp],

@@ -78,7 +78,7 @@ struct KgmtDev {
     int* R2Valid;
     int* R2Invalid;
     float* R1Score;       // [2][nR1]
-    int* delta;           // [4*nR1]: R1, R1Valid, R1Invalid, R1AvailSet of this iteration
+    unsigned long long* delta;   // [nR1]: this iteration's valid (bits 0-31) / invalid (32-63) children per R1 cell
     const float4* obstacles;
     IterCtrl* ctrl;
     PlannerStatus* status;

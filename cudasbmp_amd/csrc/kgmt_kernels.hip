@@ -81,12 +81,59 @@ __device__ __forceinline__ void block_prefix_total(const int* __restrict__ count
 // 256-slot block, workgroup-private R1 counters flushed once, R2 valid/invalid
 // counters aggregated per (cell, validity) in an LDS hash table and flushed once
 // per distinct key, and R2New bits for cells unavailable in the snapshot.
+// Add n to the count of `key` in an open-addressing LDS table.
+template <int kHash>
+__device__ __forceinline__ void hash_add(int* sKey, int* sVal, int key, int n) {
+    uint32_t h = ((uint32_t)key * 2654435761u) & (kHash - 1);
+    while (true) {
+        const int old = atomicCAS(&sKey[h], -1, key);
+        if (old == -1 || old == key) {
+            atomicAdd(&sVal[h], n);
+            return;
+        }
+        h = (h + 1) & (kHash - 1);
+    }
+}
+
+// Region counters of one wave's children, aggregated over lanes that share a key
+// before touching LDS: siblings cluster in a few cells, and per-lane atomics on one
+// LDS address serialise 64-way.  R1: one packed atomic per distinct cell (valid
+// count in bits 0-15, invalid in 16-31; a workgroup has <= 512 children).  R2: the
+// first kLeaders distinct (cell, validity) keys are aggregated, the rest added per lane.
+template <int kHash>
+__device__ __forceinline__ void count_regions(int* sR1P, int* sKey, int* sVal, int r1, int r2, bool valid) {
+    constexpr int kLeaders = 4;
+    const int lane = threadIdx.x & (kWave - 1);
+    const unsigned long long validMask = __ballot(r1 >= 0 && valid);
+    unsigned long long pending = __ballot(r1 >= 0);
+    while (pending) {
+        const int leader = __ffsll((long long)pending) - 1;
+        const int key = __builtin_amdgcn_readlane(r1, leader);
+        const unsigned long long m = __ballot(r1 == key) & pending;
+        if (lane == leader) {
+            const int nv = __popcll(m & validMask);
+            atomicAdd(&sR1P[key], nv | ((__popcll(m) - nv) << 16));
+        }
+        pending &= ~m;
+    }
+    const int key2 = (r2 >= 0) ? ((r2 << 1) | (valid ? 1 : 0)) : -1;
+    pending = __ballot(key2 >= 0);
+    for (int it = 0; it < kLeaders && pending; ++it) {
+        const int leader = __ffsll((long long)pending) - 1;
+        const int key = __builtin_amdgcn_readlane(key2, leader);
+        const unsigned long long m = __ballot(key2 == key) & pending;
+        if (lane == leader) hash_add<kHash>(sKey, sVal, key, __popcll(m));
+        pending &= ~m;
+    }
+    if ((pending >> lane) & 1ull) hash_add<kHash>(sKey, sVal, key2, 1);
+}
+
 template <int AGENT, int OBS, int CH>
 __global__ __launch_bounds__(kBlock) void k_expand(KgmtDev d, int t) {
     constexpr int kHash = 512 * CH;
     extern __shared__ float4 sObs[];
     __shared__ float sScore[kMaxR1];
-    __shared__ int sCnt[4][kMaxR1];   // R1, R1Valid, R1Invalid, R1AvailSet (workgroup-private)
+    __shared__ int sR1P[kMaxR1];      // packed (valid | invalid << 16) children per R1 cell
     __shared__ int sKey[kHash];       // (r2 << 1 | valid) -> count
     __shared__ int sVal[kHash];
     __shared__ int sWaveCnt[CH][kBlock / kWave];
@@ -132,12 +179,7 @@ __global__ __launch_bounds__(kBlock) void k_expand(KgmtDev d, int t) {
     }
 
     if (tid < d.nR1) sScore[tid] = scoreReg;
-    for (int i = tid; i < d.nR1; i += kBlock) {
-        sCnt[0][i] = 0;
-        sCnt[1][i] = 0;
-        sCnt[2][i] = 0;
-        sCnt[3][i] = 0;
-    }
+    for (int i = tid; i < d.nR1; i += kBlock) sR1P[i] = 0;
     for (int i = tid; i < kHash; i += kBlock) {
         sKey[i] = -1;
         sVal[i] = 0;
@@ -151,14 +193,15 @@ __global__ __launch_bounds__(kBlock) void k_expand(KgmtDev d, int t) {
 
 #pragma unroll
     for (int ch = 0; ch < CH; ++ch) {
-        bool accept = false;
+        bool accept = false, valid = false;
+        int r1 = -1, r2 = -1;
         if (slot[ch] < c.S) {
             Xorwow rs{ra[ch].x, ra[ch].y, ra[ch].z, ra[ch].w, rb[ch].x, rb[ch].y};
             ChildOut out;
-            const bool valid = (AGENT == 0) ? propagate_car<OBS>(p[ch], rs, d, obs, out)
-                                            : propagate_point<OBS>(p[ch], rs, d, obs, out);
-            const int r1 = getR1(out.state.x, out.state.y, d.R1Size, kN);   // N = 16 (KGMT.cu:8)
-            const int r2 = getR2(out.state.x, out.state.y, r1, d.R1Size, kN, d.R2Size, d.n);
+            valid = (AGENT == 0) ? propagate_car<OBS>(p[ch], rs, d, obs, out)
+                                 : propagate_point<OBS>(p[ch], rs, d, obs, out);
+            r1 = getR1(out.state.x, out.state.y, d.R1Size, kN);   // N = 16 (KGMT.cu:8)
+            r2 = getR2(out.state.x, out.state.y, r1, d.R1Size, kN, d.R2Size, d.n);
             if (valid) {
                 const float u = xorwow_uniform(rs);   // KGMT.cu:395
                 if (r1 >= 0 && r2 >= 0) {
@@ -166,33 +209,13 @@ __global__ __launch_bounds__(kBlock) void k_expand(KgmtDev d, int t) {
                     accept = (u <= sScore[r1]) || !r2Avail;
                 }
             }
-            // Region counters (KGMT.cu:392-411; D3: in-grid cells only).
-            if (r1 >= 0) {
-                atomicAdd(&sCnt[0][r1], 1);
-                if (valid) {
-                    atomicAdd(&sCnt[1][r1], 1);
-                    sCnt[3][r1] = 1;
-                } else {
-                    atomicAdd(&sCnt[2][r1], 1);
-                }
-            }
-            if (r2 >= 0) {
-                const int key = (r2 << 1) | (valid ? 1 : 0);
-                uint32_t h = ((uint32_t)key * 2654435761u) & (kHash - 1);
-                while (true) {
-                    const int old = atomicCAS(&sKey[h], -1, key);
-                    if (old == -1 || old == key) {
-                        atomicAdd(&sVal[h], 1);
-                        break;
-                    }
-                    h = (h + 1) & (kHash - 1);
-                }
-            }
             d.uState[slot[ch]] = out.state;
             d.uCtrl[slot[ch]] = make_float4(out.a, out.steer, out.dur, __int_as_float(parent[ch]));
             d.rngA[slot[ch]] = make_uint4(rs.v0, rs.v1, rs.v2, rs.v3);
             d.rngB[slot[ch]] = make_uint2(rs.v4, rs.d);
         }
+        // Region counters (KGMT.cu:392-411; D3: in-grid cells only).
+        count_regions<kHash>(sR1P, sKey, sVal, r1, r2, valid);
         // GNew |= accept (stale bits survive, D6).  A wave covers one 64-bit word.
         const unsigned long long mask = __ballot(accept);
         if (lane == 0) {
@@ -204,11 +227,9 @@ __global__ __launch_bounds__(kBlock) void k_expand(KgmtDev d, int t) {
     __syncthreads();
     if (tid < CH && gblock[tid] * kBlock < c.H)
         d.blockCount[gblock[tid]] = sWaveCnt[tid][0] + sWaveCnt[tid][1] + sWaveCnt[tid][2] + sWaveCnt[tid][3];
-    for (int i = tid; i < d.nR1; i += kBlock) {
-        if (sCnt[0][i]) atomicAdd(&d.delta[i], sCnt[0][i]);
-        if (sCnt[1][i]) atomicAdd(&d.delta[d.nR1 + i], sCnt[1][i]);
-        if (sCnt[2][i]) atomicAdd(&d.delta[2 * d.nR1 + i], sCnt[2][i]);
-        if (sCnt[3][i]) d.delta[3 * d.nR1 + i] = 1;
+    for (int i = tid; i < d.nR1; i += kBlock) {   // one 64-bit atomic per touched cell
+        const int v = sR1P[i];
+        if (v) atomicAdd(&d.delta[i], (unsigned long long)(v & 0xffff) | ((unsigned long long)(v >> 16) << 32));
     }
     for (int i = tid; i < kHash; i += kBlock) {
         const int key = sKey[i];
@@ -281,12 +302,15 @@ __device__ void plan_iteration(const KgmtDev& d, int t) {
     // availability snapshot for iteration t (t == 1: nothing to fold).
     for (int i = tid; i < kMaxR1; i += kBlock) sCovInc[i] = 0;
     for (int i = tid; i < d.nR1; i += kBlock) {
-        int* dl = d.delta;
-        const int a0 = dl[i], a1 = dl[d.nR1 + i], a2 = dl[2 * d.nR1 + i], a3 = dl[3 * d.nR1 + i];
-        if (a0) { d.R1[i] += a0; dl[i] = 0; }
-        if (a1) { d.R1Valid[i] += a1; dl[d.nR1 + i] = 0; }
-        if (a2) { d.R1Invalid[i] += a2; dl[2 * d.nR1 + i] = 0; }
-        if (a3) { d.R1Avail[i] = 1; dl[3 * d.nR1 + i] = 0; }
+        const unsigned long long dl = d.delta[i];
+        if (dl) {
+            const int nv = (int)(dl & 0xffffffffull), ni = (int)(dl >> 32);
+            d.R1[i] += nv + ni;            // every in-grid child (KGMT.cu:392)
+            d.R1Valid[i] += nv;            // KGMT.cu:406
+            d.R1Invalid[i] += ni;          // KGMT.cu:409
+            if (nv) d.R1Avail[i] = 1;      // KGMT.cu:399-401
+            d.delta[i] = 0ull;
+        }
     }
     __syncthreads();
     const int nn = d.n * d.n;
@@ -492,6 +516,14 @@ __global__ __launch_bounds__(kBlock) void k_init_slots(KgmtDev d, Xorwow base, c
     d.uCtrl[slot] = make_float4(0.0f, 0.0f, 0.0f, __int_as_float(-1));
 }
 
+// Holds the stream for `ticks` of the 100 MHz constant clock (bounded by
+// construction), so launches queued behind it run back to back.
+__global__ void k_delay(long long ticks) {
+    if (threadIdx.x != 0) return;
+    const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
+    while ((long long)__builtin_amdgcn_s_memrealtime() - t0 < ticks) __builtin_amdgcn_s_sleep(127);
+}
+
 // Root row and root region seeds (KGMT.cu:85-97).
 __global__ void k_seed_root(KgmtDev d, float4 rootState, float4 rootCtrl, int r1, int r2) {
     if (threadIdx.x != 0 || blockIdx.x != 0) return;
@@ -588,6 +620,11 @@ void launch_fill_f32(float* p, float v, long long n, hipStream_t s) {
 void launch_init_slots(const KgmtDev& d, const Xorwow& base, const uint32_t* jumps, int nbits, int blocks,
                        hipStream_t s) {
     hipLaunchKernelGGL(k_init_slots, dim3(blocks), dim3(kBlock), 0, s, d, base, jumps, nbits);
+}
+
+void launch_delay(double microseconds, hipStream_t s) {
+    const long long ticks = (long long)(microseconds * 100.0);   // s_memrealtime runs at 100 MHz
+    hipLaunchKernelGGL(k_delay, dim3(1), dim3(64), 0, s, ticks);
 }
 
 void launch_seed_root(const KgmtDev& d, float4 rs, float4 rc, int r1, int r2, hipStream_t s) {

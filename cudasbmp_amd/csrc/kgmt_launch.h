@@ -25,6 +25,7 @@ void launch_expand(const KgmtDev& d, int t, int agent, int blocks, int variant, 
 // t = 0 prepares iteration 1 only (insertBlocks = 0).
 void launch_finish(const KgmtDev& d, int t, int insertBlocks, hipStream_t s,
                    const KernelTiming& tm = KernelTiming());
+void launch_delay(double microseconds, hipStream_t s);
 void launch_fill_i32(int* p, int v, long long n, hipStream_t s);
 void launch_fill_f32(float* p, float v, long long n, hipStream_t s);
 void launch_init_slots(const KgmtDev& d, const Xorwow& base, const uint32_t* jumps, int nbits, int blocks,

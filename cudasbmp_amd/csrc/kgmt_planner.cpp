@@ -116,7 +116,7 @@ KgmtPlanner::KgmtPlanner(const sbmp_kgmt_params& p, int nranks, int rank, Exchan
     d.R2Valid = alloc<int>(d.nR2);
     d.R2Invalid = alloc<int>(d.nR2);
     d.R1Score = alloc<float>(2 * d.nR1);
-    d.delta = alloc<int>(4 * d.nR1);
+    d.delta = alloc<unsigned long long>(d.nR1);
     d.ctrl = alloc<IterCtrl>(p.numIterations + 2);
     d.status = alloc<PlannerStatus>(1);
     jumps_ = alloc<uint32_t>((size_t)nbits_ * 800);
@@ -162,7 +162,7 @@ void KgmtPlanner::begin(const float* initial, const float* goal, const float* d_
     SBMP_HIP(hipMemsetAsync(d.R2Valid, 0, sizeof(int) * d.nR2, s));
     SBMP_HIP(hipMemsetAsync(d.R2Invalid, 0, sizeof(int) * d.nR2, s));
     launch_fill_f32(d.R1Score, 1.0f, 2 * d.nR1, s);
-    SBMP_HIP(hipMemsetAsync(d.delta, 0, sizeof(int) * (4 * d.nR1), s));
+    SBMP_HIP(hipMemsetAsync(d.delta, 0, sizeof(unsigned long long) * d.nR1, s));
     SBMP_HIP(hipMemsetAsync(d.ctrl, 0, sizeof(IterCtrl) * (p_.numIterations + 2), s));
 
     // Obstacles: a private float4 copy of the caller's device array (KGMT.cu:80 takes

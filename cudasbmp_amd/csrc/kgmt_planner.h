@@ -60,6 +60,7 @@ public:
     std::vector<sbmp_kernel_stat> kernel_stats();
     void reset_kernel_stats();
     void set_profiling(bool on) { p_.profileKernels = on ? 1 : 0; }
+    void enqueue_delay(double us) { launch_delay(us, stream_); }
     std::vector<float> kernel_samples(const std::string& name);
 
     // sharded pieces (kgmt_sharded.cpp)

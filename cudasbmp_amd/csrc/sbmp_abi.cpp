@@ -293,6 +293,14 @@ sbmp_status sbmp_kgmt_reset_kernel_stats(sbmp_kgmt* h) {
     });
 }
 
+sbmp_status sbmp_kgmt_enqueue_delay(sbmp_kgmt* h, double microseconds) {
+    return guarded([&] {
+        PLANNER(h);
+        REQUIRE(microseconds >= 0.0 && microseconds <= 1e6, "delay must be in [0, 1 s]");
+        P.enqueue_delay(microseconds);
+    });
+}
+
 sbmp_status sbmp_kgmt_kernel_samples(sbmp_kgmt* h, const char* name, float* out, int capacity, int* count) {
     return guarded([&] {
         PLANNER(h);

@@ -275,5 +275,9 @@ class KGMT:
                  cnt.value, ctypes.byref(cnt))
         return out[: cnt.value]
 
+    def enqueue_delay(self, microseconds: float) -> None:
+        """Hold the stream for a bounded time so the launches queued next run back to back."""
+        nat.call("sbmp_kgmt_enqueue_delay", self._h, float(microseconds))
+
     def set_profiling(self, enabled: bool) -> None:
         nat.call("sbmp_kgmt_set_profiling", self._h, int(bool(enabled)))

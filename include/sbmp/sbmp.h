@@ -150,6 +150,9 @@ sbmp_status sbmp_kgmt_kernel_stats(sbmp_kgmt* h, sbmp_kernel_stat* out, int capa
 sbmp_status sbmp_kgmt_reset_kernel_stats(sbmp_kgmt* h);
 /* Turn per-launch HIP-event timing on/off for subsequently enqueued iterations. */
 sbmp_status sbmp_kgmt_set_profiling(sbmp_kgmt* h, int enabled);
+/* Queue a device-side delay (bounded spin on the GPU clock) so that the
+ * launches enqueued after it execute back to back, as in an un-instrumented run. */
+sbmp_status sbmp_kgmt_enqueue_delay(sbmp_kgmt* h, double microseconds);
 /* Individual launch durations (ms, launch order) of kernel `name` since the last reset. */
 sbmp_status sbmp_kgmt_kernel_samples(sbmp_kgmt* h, const char* name, float* out, int capacity, int* count);
 

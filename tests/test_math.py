@@ -1,0 +1,85 @@
+"""The shared deterministic transcendentals (include/sbmp/sbmp_math.h, decision D9).
+
+Run through the oracle build (same header the kernels include).  Accuracy is
+checked against float64 libm; the 2/pi table is re-derived with exact integer
+arithmetic."""
+from decimal import Decimal, getcontext
+
+import numpy as np
+import pytest
+
+
+@pytest.fixture(scope="module")
+def po(oracle_lib):
+    return oracle_lib
+
+
+def ulp_err(got, ref):
+    got = got.astype(np.float64)
+    rf = ref.astype(np.float32)
+    spacing = np.spacing(np.abs(rf)).astype(np.float64)
+    spacing[spacing == 0] = np.float64(np.float32(1e-45))
+    return np.abs(got - ref) / spacing
+
+
+@pytest.mark.parametrize("R", [0.7853, 4.0, 100.0, 1e4, 1.05e5, 1e6, 1e9, 1e20, 3e38])
+def test_sincos_accuracy(po, R):
+    rng = np.random.default_rng(int(R) % 1000 + 7)
+    x = rng.uniform(-R, R, 200_000).astype(np.float32)
+    s, c = po.sincosf(x)
+    xs = x.astype(np.float64)
+    assert ulp_err(s, np.sin(xs)).max() <= 2.0
+    assert ulp_err(c, np.cos(xs)).max() <= 2.0
+
+
+@pytest.mark.parametrize("R", [0.7853, 3.2, 100.0, 1e5, 1e9])
+def test_tan_accuracy(po, R):
+    rng = np.random.default_rng(int(R) % 1000 + 11)
+    x = rng.uniform(-R, R, 200_000).astype(np.float32)
+    t = po.tanf(x)
+    ref = np.tan(x.astype(np.float64))
+    keep = np.abs(ref) < 1e6   # near the poles the float argument itself is the error
+    assert ulp_err(t[keep], ref[keep]).max() <= 3.0
+
+
+def test_special_values(po):
+    x = np.array([0.0, -0.0, np.inf, -np.inf, np.nan], dtype=np.float32)
+    s, c = po.sincosf(x)
+    t = po.tanf(x)
+    assert s[0] == 0.0 and c[0] == 1.0 and t[0] == 0.0
+    assert np.isnan(s[2:]).all() and np.isnan(c[2:]).all() and np.isnan(t[2:]).all()
+
+
+def test_steering_range_tan_is_finite(po):
+    # Steering is drawn in (-pi, pi] (statePropagator.cu:18); tan must stay finite there.
+    x = np.nextafter(np.float32(np.pi / 2), np.float32(0)) + np.arange(-4, 5, dtype=np.float32) * np.float32(1e-7)
+    assert np.isfinite(po.tanf(x.astype(np.float32))).all()
+
+
+def _two_over_pi_words(n_words=7):
+    getcontext().prec = 120
+    # Machin: pi = 16 atan(1/5) - 4 atan(1/239), evaluated in Decimal.
+    def atan_inv(k):
+        x = Decimal(1) / k
+        x2, term, s, n = x * x, x, Decimal(0), 0
+        while True:
+            t = term / (2 * n + 1)
+            if t == 0:
+                break
+            s += t if n % 2 == 0 else -t
+            term *= x2
+            n += 1
+            if n > 400:
+                break
+        return s
+    pi = 16 * atan_inv(5) - 4 * atan_inv(239)
+    v = int((Decimal(2) / pi) * (Decimal(2) ** (32 * n_words)))
+    return [(v >> (32 * (n_words - 1 - i))) & 0xFFFFFFFF for i in range(n_words)]
+
+
+def test_two_over_pi_table_matches_integer_derivation():
+    import re
+    from conftest import ROOT
+    text = open(f"{ROOT}/include/sbmp/sbmp_math.h").read()
+    words = [int(w, 16) for w in re.findall(r"return (0x[0-9A-F]{8})u;", text)]
+    assert words == _two_over_pi_words(len(words))
