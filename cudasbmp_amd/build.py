@@ -29,6 +29,10 @@ ARCH = os.environ.get("SBMP_OFFLOAD_ARCH", "gfx950")
 COMMON = [
     "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-fno-fast-math",
     "-fhip-fp32-correctly-rounded-divide-sqrt",
+    # The SLP vectoriser packs the per-obstacle hit bits of the Euler step into
+    # 16-bit integer vectors (~25 extra VALU per step); float pairs that should be
+    # packed are written as float2 by hand (kgmt_device.h sincos_poly2).
+    "-fno-slp-vectorize",
     f"--offload-arch={ARCH}",
     "-I", os.path.join(ROOT, "include"), "-I", CSRC,
     "-Wall", "-Wno-unused-result",

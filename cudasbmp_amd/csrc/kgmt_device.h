@@ -50,6 +50,18 @@ struct PlannerStatus {
 };
 
 constexpr int kMaxLdsObs = 2048;     // obstacle lists up to 32 KB are staged in LDS per block
+// Obstacle-list forms of k_expand (template parameter OBS):
+constexpr int kObsGlobal = 0;        // read from global memory, reference early exit (> kMaxLdsObs boxes)
+constexpr int kObsLds = 1;           // staged in LDS, rolled loop
+constexpr int kObsLds4 = 2;          // staged in LDS, 4-way batched reads
+constexpr int kObsReg = 16;          // kObsReg + n: exactly n <= kMaxRegObs boxes held in registers
+constexpr int kMaxRegObs = 8;
+constexpr int obs_in_registers(int obs) { return obs >= kObsReg ? obs - kObsReg : 0; }
+constexpr int kTimelineStamps = 8;   // s_memrealtime stamps per k_expand wave (diagnostics)
+constexpr int kFoldEvery = 16;       // iterations per R2 key-log fold (k_fold_r2)
+constexpr int kFoldKeys = 65280;     // keys per fold workgroup (< 2^16: packed 16-bit LDS counters)
+constexpr int kLogMaxR2 = 32767;     // the 16-bit key (r2 | valid << 15) holds r2 < 32767
+constexpr uint16_t kNoKey = 0xffff;  // child outside the R2 grid (D3)
 
 // Everything a kernel needs, passed by value.
 struct KgmtDev {
@@ -79,9 +91,15 @@ struct KgmtDev {
     int* R2Invalid;
     float* R1Score;       // [2][nR1]
     unsigned long long* delta;   // [nR1]: this iteration's valid (bits 0-31) / invalid (32-63) children per R1 cell
+    uint16_t* r2log;      // [kFoldEvery][logSlots] per-child R2 keys (null when nR2 > kLogMaxR2)
+    int logSlots;         // this rank's slots per log row
     const float4* obstacles;
     IterCtrl* ctrl;
     PlannerStatus* status;
+    // Diagnostics (tools/timeline.py): when non-null, lane 0 of every k_expand wave of
+    // iteration timelineIter stores s_memrealtime stamps at its phase boundaries.
+    long long* timeline;
+    int timelineIter;
 };
 
 // ---------------------------------------------------------------- grid binning
@@ -135,29 +153,36 @@ SBMP_HD float xorwow_uniform(Xorwow& s) {
 // ---------------------------------------------------------------- collision
 // reference collisionCheck.cu:6-28: a segment AABB is free of an obstacle box
 // iff separated on some axis; the motion is valid iff free of every box.
-// OBS > 0: the list is staged in LDS and every box is tested without early
-// exit (independent broadcast reads, no load->compare->branch chain; the result
-// is an order-independent OR, so identical to the reference's early return).
-// Otherwise the list is read from global memory with the reference's early exit.
-__device__ __forceinline__ int box_overlap(float minx, float miny, float maxx, float maxy, float4 o) {
+// Register and LDS forms test every box without early exit (no load->compare->
+// branch chain; the result is an order-independent OR, so identical to the
+// reference's early return); the global form keeps the reference's early exit.
+__device__ __forceinline__ bool box_overlap(float minx, float miny, float maxx, float maxy, float4 o) {
     // (xmin, ymin, xmax, ymax).  !(a <= b), not (a > b): identical to the reference's
-    // predicate for NaN too.  Bitwise, not short-circuit: one 16-B read, four compares.
-    return (int)!(maxx <= o.x) & (int)!(o.z <= minx) & (int)!(maxy <= o.y) & (int)!(o.w <= miny);
+    // predicate for NaN too.  Bitwise, not short-circuit: four compares whose lane
+    // masks are combined with scalar ANDs.
+    return !(maxx <= o.x) & !(o.z <= minx) & !(maxy <= o.y) & !(o.w <= miny);
 }
 
-// OBS: 0 = global list, reference early exit; 1 = LDS list, rolled loop;
-//      2 = LDS list, 4-way unrolled (reads batched, more VGPRs).
+// OBS: kObsGlobal, kObsLds, kObsLds4, or kObsReg + n (obs points at a kernel-local
+// array of exactly n boxes: the loop is unrolled with no per-box guard, so the hit
+// mask is combined with plain scalar ANDs/ORs).
 template <int OBS>
 __device__ __forceinline__ bool motion_valid(float minx, float miny, float maxx, float maxy,
                                              const float4* __restrict__ obs, int nObs) {
-    if (OBS == 1) {
-        int hit = 0;
+    if (OBS >= kObsReg) {
+        bool hit = false;
+#pragma unroll
+        for (int i = 0; i < obs_in_registers(OBS); ++i) hit |= box_overlap(minx, miny, maxx, maxy, obs[i]);
+        return !hit;
+    }
+    if (OBS == kObsLds) {
+        bool hit = false;
 #pragma unroll 1
         for (int i = 0; i < nObs; ++i) hit |= box_overlap(minx, miny, maxx, maxy, obs[i]);
-        return hit == 0;
+        return !hit;
     }
-    if (OBS == 2) {
-        int hit = 0;
+    if (OBS == kObsLds4) {
+        bool hit = false;
         int i = 0;
         for (; i + 4 <= nObs; i += 4) {
             const float4 a = obs[i], b = obs[i + 1], c = obs[i + 2], e = obs[i + 3];
@@ -166,7 +191,7 @@ __device__ __forceinline__ bool motion_valid(float minx, float miny, float maxx,
         }
 #pragma unroll 1
         for (; i < nObs; ++i) hit |= box_overlap(minx, miny, maxx, maxy, obs[i]);
-        return hit == 0;
+        return !hit;
     }
     for (int i = 0; i < nObs; ++i) {
         const float4 o = obs[i];
@@ -176,16 +201,83 @@ __device__ __forceinline__ bool motion_valid(float minx, float miny, float maxx,
     return true;
 }
 
+// One v_min_f32 / v_max_f32: fminf / fmaxf (and fmed3 against +-inf, which the
+// compiler folds into them) add a canonicalising v_max per operand in IEEE mode.
+__device__ __forceinline__ float seg_min(float a, float b) {
+    float r;
+    asm("v_min_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+__device__ __forceinline__ float seg_max(float a, float b) {
+    float r;
+    asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+
 struct ChildOut {
     float4 state;   // x, y, theta, v
     float a, steer, dur;
 };
+
+// sincosf_d (sbmp_math.h) for the device loop: the Cody-Waite reduction, both
+// polynomials and the quadrant fix-up run on every lane; only if some lane has
+// |x| > 105615, inf or NaN does the wave enter the branch that recomputes those
+// lanes (Payne-Hanek reduction, or x - x).  Bitwise equal to sincosf_d for every x.
+// sin_poly and cos_poly (sbmp_math.h) evaluated as one float2 chain: every
+// component sees the same fused operations in the same order (so the same bits),
+// and the pair issues as packed v_pk_fma_f32 / v_pk_mul_f32.
+typedef float sbmp_f32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void sincos_poly2(float r, float* sp, float* cp) {
+    const float z = r * r;
+    const sbmp_f32x2 zz = {z, z};
+    sbmp_f32x2 p = __builtin_elementwise_fma(sbmp_f32x2{-1.9515295891e-4f, 2.443315711809948e-5f}, zz,
+                                             sbmp_f32x2{8.3321608736e-3f, -1.388731625493765e-3f});
+    p = __builtin_elementwise_fma(p, zz, sbmp_f32x2{-1.6666654611e-1f, 4.166664568298827e-2f});
+    const sbmp_f32x2 pz = p * zz;
+    const sbmp_f32x2 res = __builtin_elementwise_fma(pz, sbmp_f32x2{r, z},
+                                                     sbmp_f32x2{r, __builtin_fmaf(-0.5f, z, 1.0f)});
+    *sp = res.x;
+    *cp = res.y;
+}
+
+__device__ __forceinline__ void sincos_quadrant(float r, int q, float* s, float* c) {
+    float sp, cp;
+    sincos_poly2(r, &sp, &cp);
+    const bool odd = (q & 1) != 0;
+    const float s0 = odd ? cp : sp;
+    const float c0 = odd ? sp : cp;
+    *s = u2f(f2u(s0) ^ ((uint32_t)(q & 2) << 30));
+    *c = u2f(f2u(c0) ^ ((uint32_t)((q + 1) & 2) << 30));
+}
+
+__device__ __forceinline__ void sincos_pred(float x, float* s, float* c) {
+    const float j = __builtin_rintf(x * 0.636619772f);
+    float r = __builtin_fmaf(j, -1.57079601e+00f, x);
+    r = __builtin_fmaf(j, -3.13916473e-07f, r);
+    r = __builtin_fmaf(j, -5.39030253e-15f, r);
+    sincos_quadrant(r, (int)j, s, c);
+    if (!(__builtin_fabsf(x) <= 105615.0f)) {   // rare: huge, inf or NaN argument
+        if (finitef(x)) {
+            int q;
+            const float rh = reduce_payne_hanek(x, &q);
+            sincos_quadrant(rh, q, s, c);
+        } else {
+            *s = x - x;
+            *c = x - x;
+        }
+    }
+}
 
 // reference statePropagator.cu:5-76 (car).  Same operation sequence as the oracle
 // (D9-D11): fmaf where nvcc would contract, steering via one double fma.
 // v / agentLength: when agentLength is a power of two, v * (1/agentLength) is the
 // same correctly rounded value (both are the exact product scaled by 2^-k), so the
 // host passes invAgentLength != 0 and the per-step division disappears.
+// Predicated instead of the reference's per-lane break: every live lane computes
+// the step; a lane that fails the bounds test keeps its new (x, y) and its old
+// (theta, v), a lane that fails the collision test keeps all four (exactly the
+// state at the reference's break), and later steps leave a dead lane unchanged.
+// The wave leaves the loop once no lane is alive.
 template <int OBS>
 __device__ __forceinline__ bool propagate_car(float4 p, Xorwow& rs, const KgmtDev& d, const float4* obs,
                                               ChildOut& out) {
@@ -196,35 +288,38 @@ __device__ __forceinline__ bool propagate_car(float4 p, Xorwow& rs, const KgmtDe
     const float dt = duration / (float)d.numDisc;
     float x = p.x, y = p.y, theta = p.z, v = p.w;
     const float tan_steering = tanf_d(steering);
-    bool valid = true;
+    bool alive = true;
     for (int i = 0; i < d.numDisc; ++i) {
-        const float px = x, py = y;
         float st, ct;
-        sincosf_d(theta, &st, &ct);
-        x = __builtin_fmaf(v * ct, dt, x);
-        y = __builtin_fmaf(v * st, dt, y);
-        if (x <= 0.0f || x >= d.width || y <= 0.0f || y >= d.height) {
-            valid = false;
-            break;
-        }
+        sincos_pred(theta, &st, &ct);
+        const float nx = __builtin_fmaf(v * ct, dt, x);
+        const float ny = __builtin_fmaf(v * st, dt, y);
+        const bool oob = (nx <= 0.0f) | (nx >= d.width) | (ny <= 0.0f) | (ny >= d.height);
         const float vl = (d.invAgentLength != 0.0f) ? v * d.invAgentLength : v / d.agentLength;
-        theta = __builtin_fmaf(vl * tan_steering, dt, theta);
-        v = __builtin_fmaf(a, dt, v);
-        const float minx = (px > x) ? x : px, maxx = (px > x) ? px : x;
-        const float miny = (py > y) ? y : py, maxy = (py > y) ? py : y;
-        if (!motion_valid<OBS>(minx, miny, maxx, maxy, obs, d.nObs)) {
-            valid = false;
-            break;
-        }
+        const float nth = __builtin_fmaf(vl * tan_steering, dt, theta);
+        const float nv = __builtin_fmaf(a, dt, v);
+        // (x > nx ? nx : x) etc. as one v_min / v_max.  They differ from the ternaries
+        // only for NaN operands, which need a non-finite theta or v: begin() rejects a
+        // non-finite root, and finite states stay finite.
+        const float minx = seg_min(x, nx), maxx = seg_max(x, nx);
+        const float miny = seg_min(y, ny), maxy = seg_max(y, ny);
+        const bool freeSeg = motion_valid<OBS>(minx, miny, maxx, maxy, obs, d.nObs);
+        const bool adv = alive & !oob;
+        x = alive ? nx : x;
+        y = alive ? ny : y;
+        theta = adv ? nth : theta;
+        v = adv ? nv : v;
+        alive = adv & freeSeg;
+        if (__ballot(alive) == 0ull) break;
     }
     out.state = make_float4(x, y, theta, v);
     out.a = a;
     out.steer = steering;
     out.dur = duration;
-    return valid;
+    return alive;
 }
 
-// Holonomic R2 point (build extension).
+// Holonomic R2 point (build extension), predicated like propagate_car.
 template <int OBS>
 __device__ __forceinline__ bool propagate_point(float4 p, Xorwow& rs, const KgmtDev& d, const float4* obs,
                                                 ChildOut& out) {
@@ -233,27 +328,24 @@ __device__ __forceinline__ bool propagate_point(float4 p, Xorwow& rs, const Kgmt
     const float duration = __builtin_fmaf(xorwow_uniform(rs), 1.0f, 0.05f);
     const float dt = duration / (float)d.numDisc;
     float x = p.x, y = p.y;
-    bool valid = true;
+    bool alive = true;
     for (int i = 0; i < d.numDisc; ++i) {
-        const float px = x, py = y;
-        x = __builtin_fmaf(vx, dt, x);
-        y = __builtin_fmaf(vy, dt, y);
-        if (x <= 0.0f || x >= d.width || y <= 0.0f || y >= d.height) {
-            valid = false;
-            break;
-        }
-        const float minx = (px > x) ? x : px, maxx = (px > x) ? px : x;
-        const float miny = (py > y) ? y : py, maxy = (py > y) ? py : y;
-        if (!motion_valid<OBS>(minx, miny, maxx, maxy, obs, d.nObs)) {
-            valid = false;
-            break;
-        }
+        const float nx = __builtin_fmaf(vx, dt, x);
+        const float ny = __builtin_fmaf(vy, dt, y);
+        const bool oob = (nx <= 0.0f) | (nx >= d.width) | (ny <= 0.0f) | (ny >= d.height);
+        const float minx = seg_min(x, nx), maxx = seg_max(x, nx);   // see propagate_car
+        const float miny = seg_min(y, ny), maxy = seg_max(y, ny);
+        const bool freeSeg = motion_valid<OBS>(minx, miny, maxx, maxy, obs, d.nObs);
+        x = alive ? nx : x;
+        y = alive ? ny : y;
+        alive = alive & !oob & freeSeg;
+        if (__ballot(alive) == 0ull) break;
     }
     out.state = make_float4(x, y, 0.0f, 0.0f);
     out.a = vx;
     out.steer = vy;
     out.dur = duration;
-    return valid;
+    return alive;
 }
 
 }  // namespace sbmp

@@ -43,6 +43,39 @@ __device__ __forceinline__ int div_small(int a, int b) {
     return q;
 }
 
+// The 64-B control block of one iteration with ONE scalar load.  The compiler
+// reads it with vector loads (the launch also stores ctrl[t].executed, so it
+// cannot prove the line unclobbered, and it folds a constant-address-space cast
+// back to global): each then waits with vmcnt(0) behind every older vector load
+// (XORWOW states, snapshot words), which serialised the prologue.  A scalar load
+// waits on lgkmcnt only.  The fields read here are written by the previous launch;
+// this launch writes only .executed, which it never reads.  The "memory" clobber
+// keeps the independent vector loads issued above it.
+// The goal status (written by earlier launches only) comes with it.
+typedef int sbmp_i32x16 __attribute__((ext_vector_type(16)));
+__device__ __forceinline__ IterCtrl load_ctrl(const IterCtrl* p, const PlannerStatus* st, int* goalIdx) {
+    sbmp_i32x16 v;
+    int g;
+    asm volatile("s_load_dwordx16 %0, %2, 0x0\n\ts_load_dword %1, %3, 0x0\n\ts_waitcnt lgkmcnt(0)"
+                 : "=s"(v), "=s"(g)
+                 : "s"(p), "s"(st)
+                 : "memory");
+    *goalIdx = g;
+    IterCtrl c;
+    c.run = v[0];
+    c.executed = v[1];
+    c.treeSize = v[2];
+    c.gLo = v[3];
+    c.nG = v[4];
+    c.k = v[5];
+    c.nExp = v[6];
+    c.S = v[7];
+    c.H = v[8];
+    c.A = v[9];
+    c.scoreBuf = v[10];
+    return c;
+}
+
 __device__ __forceinline__ int wave_sum(int v) {
 #pragma unroll
     for (int off = kWave / 2; off > 0; off >>= 1) v += __shfl_xor(v, off, kWave);
@@ -73,175 +106,181 @@ __device__ __forceinline__ void block_prefix_total(const int* __restrict__ count
 }
 
 // ------------------------------------------------------------------ expand
-// One thread per child slot.  A workgroup of 256 threads processes CH ownership
-// blocks of 256 slots each (CH chunks): the XORWOW states of all its chunks are
-// loaded up front, so the stores of chunk c drain while chunk c+1 computes.
-// Outputs: child state/controls/parent (2 x 16 B), XORWOW state (16 + 8 B),
-// GNew bits (one 8-B word per wave and chunk), the GNew popcount of each
-// 256-slot block, workgroup-private R1 counters flushed once, R2 valid/invalid
-// counters aggregated per (cell, validity) in an LDS hash table and flushed once
-// per distinct key, and R2New bits for cells unavailable in the snapshot.
-// Add n to the count of `key` in an open-addressing LDS table.
-template <int kHash>
-__device__ __forceinline__ void hash_add(int* sKey, int* sVal, int key, int n) {
-    uint32_t h = ((uint32_t)key * 2654435761u) & (kHash - 1);
-    while (true) {
-        const int old = atomicCAS(&sKey[h], -1, key);
-        if (old == -1 || old == key) {
-            atomicAdd(&sVal[h], n);
-            return;
-        }
-        h = (h + 1) & (kHash - 1);
-    }
-}
-
-// Region counters of one wave's children, aggregated over lanes that share a key
-// before touching LDS: siblings cluster in a few cells, and per-lane atomics on one
-// LDS address serialise 64-way.  R1: one packed atomic per distinct cell (valid
-// count in bits 0-15, invalid in 16-31; a workgroup has <= 512 children).  R2: the
-// first kLeaders distinct (cell, validity) keys are aggregated, the rest added per lane.
-template <int kHash>
-__device__ __forceinline__ void count_regions(int* sR1P, int* sKey, int* sVal, int r1, int r2, bool valid) {
-    constexpr int kLeaders = 4;
-    const int lane = threadIdx.x & (kWave - 1);
-    const unsigned long long validMask = __ballot(r1 >= 0 && valid);
-    unsigned long long pending = __ballot(r1 >= 0);
-    while (pending) {
-        const int leader = __ffsll((long long)pending) - 1;
-        const int key = __builtin_amdgcn_readlane(r1, leader);
-        const unsigned long long m = __ballot(r1 == key) & pending;
-        if (lane == leader) {
-            const int nv = __popcll(m & validMask);
-            atomicAdd(&sR1P[key], nv | ((__popcll(m) - nv) << 16));
-        }
-        pending &= ~m;
-    }
-    const int key2 = (r2 >= 0) ? ((r2 << 1) | (valid ? 1 : 0)) : -1;
-    pending = __ballot(key2 >= 0);
-    for (int it = 0; it < kLeaders && pending; ++it) {
-        const int leader = __ffsll((long long)pending) - 1;
-        const int key = __builtin_amdgcn_readlane(key2, leader);
-        const unsigned long long m = __ballot(key2 == key) & pending;
-        if (lane == leader) hash_add<kHash>(sKey, sVal, key, __popcll(m));
-        pending &= ~m;
-    }
-    if ((pending >> lane) & 1ull) hash_add<kHash>(sKey, sVal, key2, 1);
-}
-
-template <int AGENT, int OBS, int CH>
+// One thread per child slot, 256-slot workgroups.  Outputs: child state/controls/
+// parent (2 x 16 B), XORWOW state (16 + 8 B), GNew bits (one 8-B word per wave),
+// the GNew popcount of the workgroup, and the region bookkeeping of
+// KGMT.cu:392-411 (D3: in-grid cells only):
+//   R1 counts   workgroup-private packed LDS counters (valid | invalid << 16), one
+//               64-bit device atomic per touched cell;
+//   R2New       availability bits of cells seen valid while unavailable in the
+//               snapshot: an LDS bitmask, one device atomicOr per nonzero word;
+//   R2 counts   one 16-bit key (r2 | valid << 15) per child into the key log, folded
+//               into R2Valid / R2Invalid every kFoldEvery iterations (k_fold_r2).
+//               Siblings scatter over ~150 distinct R2 cells per workgroup, and
+//               scattered device atomics run ~17x below the contiguous rate
+//               (MI355X_MICROARCH.md, global atomics); nothing reads these two
+//               arrays during the run (KGMT.cu:405,410 are write-only).
+template <int AGENT, int OBS>
 __global__ __launch_bounds__(kBlock) void k_expand(KgmtDev d, int t) {
-    constexpr int kHash = 512 * CH;
     extern __shared__ float4 sObs[];
     __shared__ float sScore[kMaxR1];
-    __shared__ int sR1P[kMaxR1];      // packed (valid | invalid << 16) children per R1 cell
-    __shared__ int sKey[kHash];       // (r2 << 1 | valid) -> count
-    __shared__ int sVal[kHash];
-    __shared__ int sWaveCnt[CH][kBlock / kWave];
+    __shared__ int sR1P[kMaxR1];
+    __shared__ uint32_t sSnap[kMaxR2Words];   // R2 availability at the iteration start (D2)
+    __shared__ uint32_t sNew[kMaxR2Words];
+    __shared__ int sWaveCnt[kBlock / kWave];
 
     const int tid = threadIdx.x;
     const int lane = tid & (kWave - 1);
     const int wave = tid >> 6;
-    int gblock[CH], slot[CH];
+    long long* const tl = (d.timeline && t == d.timelineIter)
+                              ? d.timeline + ((size_t)blockIdx.x * (kBlock / kWave) + wave) * kTimelineStamps
+                              : nullptr;
+#define SBMP_STAMP(i)                                                                  \
+    do {                                                                               \
+        if (tl && lane == 0) tl[i] = (long long)__builtin_amdgcn_s_memrealtime();      \
+    } while (0)
+    // Entry stamp kept in a register: a store here would make every later load a
+    // possible alias of it.
+    const long long entryStamp = tl ? (long long)__builtin_amdgcn_s_memrealtime() : 0;
+    constexpr bool kLdsObs = (OBS == kObsLds || OBS == kObsLds4);
+    constexpr int kRegObs = obs_in_registers(OBS);
+    float4 ro[kRegObs > 0 ? kRegObs : 1];   // register-resident obstacle list
 #pragma unroll
-    for (int ch = 0; ch < CH; ++ch) {
-        gblock[ch] = d.rank + d.nranks * ((int)blockIdx.x * CH + ch);   // block-cyclic slot ownership
-        slot[ch] = gblock[ch] * kBlock + tid;
-    }
+    for (int i = 0; i < kRegObs; ++i) ro[i] = d.obstacles[i];
+    const int gblock = d.rank + d.nranks * (int)blockIdx.x;   // block-cyclic slot ownership
+    const int slot = gblock * kBlock + tid;
+    const int nW = d.nR2 >> 5;
 
-    // Latency: issue every load that does not depend on the control block before
-    // waiting for it (slot arrays are allocated to a whole number of workgroups; the
-    // score buffer of iteration t is t & 1).  Only the parent-row loads wait on ctrl.
-    uint4 ra[CH];
-    uint2 rb[CH];
-    unsigned long long oldWord[CH];
-#pragma unroll
-    for (int ch = 0; ch < CH; ++ch) {
-        ra[ch] = d.rngA[slot[ch]];
-        rb[ch] = d.rngB[slot[ch]];
-        oldWord[ch] = (lane == 0) ? d.gnew[slot[ch] >> 6] : 0ull;
-    }
+    // Latency: every load that does not depend on the control block is issued
+    // before it (slot arrays are allocated to a whole number of workgroups; the
+    // score buffer of iteration t is t & 1); the control block is one scalar load;
+    // the parent-row load follows it directly.
+    const uint4 ra = d.rngA[slot];
+    const uint2 rb = d.rngB[slot];
+    const unsigned long long oldWord = (lane == 0) ? d.gnew[slot >> 6] : 0ull;
     const float scoreReg = (tid < d.nR1) ? d.R1Score[(t & 1) * d.nR1 + tid] : 0.0f;
-    const float4 obsReg = (OBS > 0 && tid < d.nObs) ? d.obstacles[tid] : make_float4(0.f, 0.f, 0.f, 0.f);
-
-    const IterCtrl c = d.ctrl[t];
-    if (!c.run || d.status->goalIdx != kNoGoal) return;   // grid-uniform
-    if (blockIdx.x == 0 && threadIdx.x == 0) d.ctrl[t].executed = 1;
-    if (gblock[0] * kBlock >= c.H) return;   // past every batch and every stale bit (workgroup-uniform)
-
-    float4 p[CH];
-    int parent[CH];
+    const float4 obsReg = (kLdsObs && tid < d.nObs) ? d.obstacles[tid] : make_float4(0.f, 0.f, 0.f, 0.f);
+    uint32_t snapReg[kMaxR2Words / kBlock];
 #pragma unroll
-    for (int ch = 0; ch < CH; ++ch) {
-        const bool act = slot[ch] < c.S;
-        const int g = !act ? 0 : (c.k == 32) ? (slot[ch] >> 5) : div_small(slot[ch], c.k);   // slot = g*k + i
-        parent[ch] = c.gLo + g;
-        p[ch] = act ? d.treeState[parent[ch]] : make_float4(0.f, 0.f, 0.f, 0.f);
-    }
+    for (int j = 0; j < kMaxR2Words / kBlock; ++j) snapReg[j] = (tid + j * kBlock < nW) ? d.R2Snap[tid + j * kBlock] : 0u;
+
+    int goalIdx;
+    const IterCtrl c = load_ctrl(d.ctrl + t, d.status, &goalIdx);
+    if (!c.run || goalIdx != kNoGoal) return;   // grid-uniform
+    if (blockIdx.x == 0 && threadIdx.x == 0) d.ctrl[t].executed = 1;
+    if (gblock * kBlock >= c.H) return;   // past every batch and every stale bit (workgroup-uniform)
+
+    // Parent row, unconditional (inactive slots read row 0, which always exists): a
+    // load inside a branch makes the compiler wait with vmcnt(0) at the join, i.e.
+    // for this load too before the LDS set-up below.
+    const bool act = slot < c.S;
+    const int g = !act ? 0 : (c.k == 32) ? (slot >> 5) : div_small(slot, c.k);   // slot = g*k + i
+    const int parent = act ? c.gLo + g : 0;
+    const float4 p = d.treeState[parent];
 
     if (tid < d.nR1) sScore[tid] = scoreReg;
     for (int i = tid; i < d.nR1; i += kBlock) sR1P[i] = 0;
-    for (int i = tid; i < kHash; i += kBlock) {
-        sKey[i] = -1;
-        sVal[i] = 0;
+#pragma unroll
+    for (int j = 0; j < kMaxR2Words / kBlock; ++j) {
+        if (tid + j * kBlock < nW) {
+            sSnap[tid + j * kBlock] = snapReg[j];
+            sNew[tid + j * kBlock] = 0u;
+        }
     }
-    if (OBS > 0) {
+    if (kLdsObs) {
         if (tid < d.nObs) sObs[tid] = obsReg;
         for (int i = tid + kBlock; i < d.nObs; i += kBlock) sObs[i] = d.obstacles[i];
     }
     __syncthreads();
-    const float4* obs = (OBS > 0) ? sObs : d.obstacles;
+    if (tl && lane == 0) tl[0] = entryStamp;
+    SBMP_STAMP(1);
+    const float4* obs = (kRegObs > 0) ? ro : kLdsObs ? sObs : d.obstacles;
 
-#pragma unroll
-    for (int ch = 0; ch < CH; ++ch) {
-        bool accept = false, valid = false;
-        int r1 = -1, r2 = -1;
-        if (slot[ch] < c.S) {
-            Xorwow rs{ra[ch].x, ra[ch].y, ra[ch].z, ra[ch].w, rb[ch].x, rb[ch].y};
-            ChildOut out;
-            valid = (AGENT == 0) ? propagate_car<OBS>(p[ch], rs, d, obs, out)
-                                 : propagate_point<OBS>(p[ch], rs, d, obs, out);
-            r1 = getR1(out.state.x, out.state.y, d.R1Size, kN);   // N = 16 (KGMT.cu:8)
-            r2 = getR2(out.state.x, out.state.y, r1, d.R1Size, kN, d.R2Size, d.n);
-            if (valid) {
-                const float u = xorwow_uniform(rs);   // KGMT.cu:395
-                if (r1 >= 0 && r2 >= 0) {
-                    const bool r2Avail = (d.R2Snap[r2 >> 5] >> (r2 & 31)) & 1u;
-                    accept = (u <= sScore[r1]) || !r2Avail;
-                }
+    bool accept = false;
+    if (act) {
+        Xorwow rs{ra.x, ra.y, ra.z, ra.w, rb.x, rb.y};
+        ChildOut out;
+        const bool valid = (AGENT == 0) ? propagate_car<OBS>(p, rs, d, obs, out)
+                                        : propagate_point<OBS>(p, rs, d, obs, out);
+        SBMP_STAMP(2);
+        const int r1 = getR1(out.state.x, out.state.y, d.R1Size, kN);   // N = 16 (KGMT.cu:8)
+        const int r2 = getR2(out.state.x, out.state.y, r1, d.R1Size, kN, d.R2Size, d.n);
+        if (valid) {
+            const float u = xorwow_uniform(rs);   // KGMT.cu:395
+            if (r2 >= 0) {                        // r2 >= 0 implies r1 >= 0
+                const uint32_t bit = 1u << (r2 & 31);
+                const bool r2Avail = sSnap[r2 >> 5] & bit;
+                accept = (u <= sScore[r1]) || !r2Avail;
+                if (!r2Avail) atomicOr(&sNew[r2 >> 5], bit);
             }
-            d.uState[slot[ch]] = out.state;
-            d.uCtrl[slot[ch]] = make_float4(out.a, out.steer, out.dur, __int_as_float(parent[ch]));
-            d.rngA[slot[ch]] = make_uint4(rs.v0, rs.v1, rs.v2, rs.v3);
-            d.rngB[slot[ch]] = make_uint2(rs.v4, rs.d);
         }
-        // Region counters (KGMT.cu:392-411; D3: in-grid cells only).
-        count_regions<kHash>(sR1P, sKey, sVal, r1, r2, valid);
-        // GNew |= accept (stale bits survive, D6).  A wave covers one 64-bit word.
-        const unsigned long long mask = __ballot(accept);
-        if (lane == 0) {
-            const unsigned long long now = oldWord[ch] | mask;
-            if (now != oldWord[ch]) d.gnew[slot[ch] >> 6] = now;
-            sWaveCnt[ch][wave] = __popcll(now);   // chunks past S: the stale bits' count
+        d.uState[slot] = out.state;
+        d.uCtrl[slot] = make_float4(out.a, out.steer, out.dur, __int_as_float(parent));
+        d.rngA[slot] = make_uint4(rs.v0, rs.v1, rs.v2, rs.v3);
+        d.rngB[slot] = make_uint2(rs.v4, rs.d);
+        if (r1 >= 0) atomicAdd(&sR1P[r1], valid ? 1 : 0x10000);
+        if (d.r2log) {
+            d.r2log[(size_t)(t % kFoldEvery) * d.logSlots + (int)blockIdx.x * kBlock + tid] =
+                (r2 >= 0) ? (uint16_t)(r2 | (valid ? 0x8000 : 0)) : kNoKey;
+        } else if (r2 >= 0) {   // more than kLogMaxR2 R2 cells: direct device atomics
+            atomicAdd(valid ? &d.R2Valid[r2] : &d.R2Invalid[r2], 1);
         }
     }
+    SBMP_STAMP(3);
+    // GNew |= accept (stale bits survive, D6).  A wave covers one 64-bit word.
+    const unsigned long long mask = __ballot(accept);
+    if (lane == 0) {
+        const unsigned long long now = oldWord | mask;
+        if (now != oldWord) d.gnew[slot >> 6] = now;
+        sWaveCnt[wave] = __popcll(now);   // slots past S: the stale bits' count
+    }
+    SBMP_STAMP(4);
     __syncthreads();
-    if (tid < CH && gblock[tid] * kBlock < c.H)
-        d.blockCount[gblock[tid]] = sWaveCnt[tid][0] + sWaveCnt[tid][1] + sWaveCnt[tid][2] + sWaveCnt[tid][3];
+    SBMP_STAMP(5);
+    if (tid == 0) d.blockCount[gblock] = sWaveCnt[0] + sWaveCnt[1] + sWaveCnt[2] + sWaveCnt[3];
     for (int i = tid; i < d.nR1; i += kBlock) {   // one 64-bit atomic per touched cell
         const int v = sR1P[i];
         if (v) atomicAdd(&d.delta[i], (unsigned long long)(v & 0xffff) | ((unsigned long long)(v >> 16) << 32));
     }
-    for (int i = tid; i < kHash; i += kBlock) {
-        const int key = sKey[i];
-        if (key < 0) continue;
-        const int r2 = key >> 1;
-        if (key & 1) {
-            atomicAdd(&d.R2Valid[r2], sVal[i]);
-            const uint32_t bit = 1u << (r2 & 31);
-            if (!(d.R2Snap[r2 >> 5] & bit)) atomicOr(&d.R2New[r2 >> 5], bit);
-        } else {
-            atomicAdd(&d.R2Invalid[r2], sVal[i]);
+    for (int i = tid; i < nW; i += kBlock) {
+        const uint32_t w = sNew[i];
+        if (w) atomicOr(&d.R2New[i], w);
+    }
+    SBMP_STAMP(6);
+#undef SBMP_STAMP
+}
+
+// R2Valid / R2Invalid (KGMT.cu:405,410) from the key log of iteration
+// tFirst + blockIdx.y: a dense LDS histogram per workgroup (packed valid |
+// invalid << 16; a workgroup takes at most kFoldKeys < 2^16 keys, so neither half
+// overflows), flushed with one atomic per nonzero half, consecutive lanes on
+// consecutive cells.  Keys of slots >= S of that iteration are stale and skipped;
+// iterations that did not execute are skipped whole.
+__global__ __launch_bounds__(1024) void k_fold_r2(KgmtDev d, int tFirst) {
+    extern __shared__ uint32_t sCnt[];
+    const int t = tFirst + (int)blockIdx.y;
+    const IterCtrl c = d.ctrl[t];
+    if (!c.executed) return;
+    for (int i = threadIdx.x; i < d.nR2; i += blockDim.x) sCnt[i] = 0u;
+    __syncthreads();
+    const uint16_t* row = d.r2log + (size_t)(t % kFoldEvery) * d.logSlots;
+    const int begin = (int)blockIdx.x * kFoldKeys;
+    const int end = min(begin + kFoldKeys, d.logSlots);
+    for (int i = begin + (int)threadIdx.x * 8; i < end; i += (int)blockDim.x * 8) {
+        const uint4 w = *reinterpret_cast<const uint4*>(row + i);
+        const uint32_t wv[4] = {w.x, w.y, w.z, w.w};
+        const int gslot = (d.rank + d.nranks * (i >> 8)) * kBlock + (i & (kBlock - 1));   // 8 keys, one block
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const uint32_t key = (wv[j >> 1] >> ((j & 1) * 16)) & 0xffffu;
+            if (gslot + j < c.S && key != kNoKey) atomicAdd(&sCnt[key & 0x7fffu], (key & 0x8000u) ? 1u : 0x10000u);
         }
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < d.nR2; i += blockDim.x) {
+        const uint32_t v = sCnt[i];
+        if (v & 0xffffu) atomicAdd(&d.R2Valid[i], (int)(v & 0xffffu));
+        if (v >> 16) atomicAdd(&d.R2Invalid[i], (int)(v >> 16));
     }
 }
 
@@ -577,28 +616,46 @@ static void launch(K kernel, dim3 grid, dim3 block, size_t shm, hipStream_t s, c
         hipLaunchKernelGGL(kernel, grid, block, shm, s, args...);
 }
 
-template <int AGENT, int CH>
+template <int AGENT>
 static void launch_expand_agent(const KgmtDev& d, int t, int blocks, int variant, hipStream_t s,
                                 const KernelTiming& tm) {
     const size_t shm = sizeof(float4) * (size_t)d.nObs;
-    const dim3 grid(blocks / CH);
-    if (d.nObs > kMaxLdsObs)
-        launch(k_expand<AGENT, 0, CH>, grid, dim3(kBlock), 0, s, tm, d, t);
-    else if (variant == 2)
-        launch(k_expand<AGENT, 2, CH>, grid, dim3(kBlock), shm, s, tm, d, t);
-    else
-        launch(k_expand<AGENT, 1, CH>, grid, dim3(kBlock), shm, s, tm, d, t);
+    const dim3 grid(blocks), block(kBlock);
+    if (d.nObs > kMaxLdsObs) {
+        launch(k_expand<AGENT, kObsGlobal>, grid, block, 0, s, tm, d, t);
+    } else if (d.nObs <= kMaxRegObs && (variant == 0 || variant == 3)) {
+        switch (d.nObs) {   // the box count is a compile-time constant of the register path
+            case 0: launch(k_expand<AGENT, kObsReg + 0>, grid, block, 0, s, tm, d, t); break;
+            case 1: launch(k_expand<AGENT, kObsReg + 1>, grid, block, 0, s, tm, d, t); break;
+            case 2: launch(k_expand<AGENT, kObsReg + 2>, grid, block, 0, s, tm, d, t); break;
+            case 3: launch(k_expand<AGENT, kObsReg + 3>, grid, block, 0, s, tm, d, t); break;
+            case 4: launch(k_expand<AGENT, kObsReg + 4>, grid, block, 0, s, tm, d, t); break;
+            case 5: launch(k_expand<AGENT, kObsReg + 5>, grid, block, 0, s, tm, d, t); break;
+            case 6: launch(k_expand<AGENT, kObsReg + 6>, grid, block, 0, s, tm, d, t); break;
+            case 7: launch(k_expand<AGENT, kObsReg + 7>, grid, block, 0, s, tm, d, t); break;
+            default: launch(k_expand<AGENT, kObsReg + 8>, grid, block, 0, s, tm, d, t); break;
+        }
+    } else if (variant == 2) {
+        launch(k_expand<AGENT, kObsLds4>, grid, block, shm, s, tm, d, t);
+    } else {
+        launch(k_expand<AGENT, kObsLds>, grid, block, shm, s, tm, d, t);
+    }
 }
 
-void launch_expand(const KgmtDev& d, int t, int agent, int blocks, int variant, int chunks, hipStream_t s,
+void launch_expand(const KgmtDev& d, int t, int agent, int blocks, int variant, hipStream_t s,
                    const KernelTiming& tm) {
-    if (chunks == 2) {
-        if (agent == 0) launch_expand_agent<0, 2>(d, t, blocks, variant, s, tm);
-        else launch_expand_agent<1, 2>(d, t, blocks, variant, s, tm);
-    } else {
-        if (agent == 0) launch_expand_agent<0, 1>(d, t, blocks, variant, s, tm);
-        else launch_expand_agent<1, 1>(d, t, blocks, variant, s, tm);
-    }
+    if (agent == 0) launch_expand_agent<0>(d, t, blocks, variant, s, tm);
+    else launch_expand_agent<1>(d, t, blocks, variant, s, tm);
+}
+
+void launch_fold_r2(const KgmtDev& d, int tFirst, int tLast, hipStream_t s, const KernelTiming& tm) {
+    if (!d.r2log || tLast < tFirst) return;
+    const size_t shm = sizeof(uint32_t) * (size_t)d.nR2;
+    if (shm > 65536)   // dynamic LDS above 64 KB needs the opt-in (n > 8); per device, so every time
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_fold_r2),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
+    const dim3 grid((d.logSlots + kFoldKeys - 1) / kFoldKeys, tLast - tFirst + 1);
+    launch(k_fold_r2, grid, dim3(1024), shm, s, tm, d, tFirst);
 }
 
 void launch_finish(const KgmtDev& d, int t, int insertBlocks, hipStream_t s, const KernelTiming& tm) {

@@ -16,11 +16,13 @@ struct KernelTiming {
     hipEvent_t stop = nullptr;
 };
 
-// variant: obstacle-loop form for LDS-resident lists (1 = rolled, 2 = 4-way batched);
-// lists longer than kMaxLdsObs always use the global early-exit form.
-// chunks: 256-slot ownership blocks per workgroup (1 or 2; blocks % chunks == 0).
-void launch_expand(const KgmtDev& d, int t, int agent, int blocks, int variant, int chunks, hipStream_t s,
+// variant: obstacle form: 0 = auto, 1 = LDS rolled, 2 = LDS 4-way batched, 3 = registers
+// (lists of at most kMaxRegObs boxes; auto picks it there, else 1); lists longer
+// than kMaxLdsObs always use the global early-exit form.
+void launch_expand(const KgmtDev& d, int t, int agent, int blocks, int variant, hipStream_t s,
                    const KernelTiming& tm = KernelTiming());
+// k_fold_r2: add the key log of iterations [tFirst, tLast] (at most kFoldEvery) to R2Valid / R2Invalid.
+void launch_fold_r2(const KgmtDev& d, int tFirst, int tLast, hipStream_t s, const KernelTiming& tm = KernelTiming());
 // k_finish(t): insert iteration t (insertBlocks blocks) + prepare iteration t+1.
 // t = 0 prepares iteration 1 only (insertBlocks = 0).
 void launch_finish(const KgmtDev& d, int t, int insertBlocks, hipStream_t s,

@@ -57,12 +57,11 @@ KgmtPlanner::KgmtPlanner(const sbmp_kgmt_params& p, int nranks, int rank, Exchan
     if (p.device < 0 || p.device >= ndev) throw Error(SBMP_ERR_INVALID_ARGUMENT, "no such HIP device");
     SBMP_HIP(hipSetDevice(p.device));
     SBMP_HIP(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
-    if (const char* v = getenv("SBMP_EXPAND_VARIANT")) expandVariant_ = atoi(v) == 2 ? 2 : 1;
-    if (const char* v = getenv("SBMP_EXPAND_CHUNKS")) expandChunks_ = atoi(v) == 2 ? 2 : 1;
+    if (const char* v = getenv("SBMP_EXPAND_VARIANT")) expandVariant_ = std::min(3, std::max(0, atoi(v)));
 
     const int M = p.maxTreeSize;
     const int nSlots = p.samplesPerIteration > 0 ? std::min(M, p.samplesPerIteration) : M;
-    slotsPadded_ = round_up(nSlots, 2ll * kBlock * nranks);   // whole workgroups at 1 or 2 chunks
+    slotsPadded_ = round_up(nSlots, (long long)kBlock * nranks);   // whole workgroups on every rank
     expandBlocks_ = slotsPadded_ / kBlock / nranks;
     const int nWords = slotsPadded_ / kWave;
     while ((1ll << nbits_) < nSlots) ++nbits_;
@@ -117,8 +116,18 @@ KgmtPlanner::KgmtPlanner(const sbmp_kgmt_params& p, int nranks, int rank, Exchan
     d.R2Invalid = alloc<int>(d.nR2);
     d.R1Score = alloc<float>(2 * d.nR1);
     d.delta = alloc<unsigned long long>(d.nR1);
+    d.logSlots = expandBlocks_ * kBlock;
+    d.r2log = (d.nR2 <= kLogMaxR2) ? alloc<uint16_t>((size_t)kFoldEvery * d.logSlots) : nullptr;
     d.ctrl = alloc<IterCtrl>(p.numIterations + 2);
     d.status = alloc<PlannerStatus>(1);
+    d.timeline = nullptr;
+    d.timelineIter = -1;
+    if (const char* v = getenv("SBMP_TIMELINE_ITER")) {   // diagnostics: tools/timeline.py
+        d.timelineIter = atoi(v);
+        d.timeline = alloc<long long>((size_t)expandBlocks_ * (kBlock / kWave) * kTimelineStamps);
+        SBMP_HIP(hipMemsetAsync(d.timeline, 0,
+                                sizeof(long long) * expandBlocks_ * (kBlock / kWave) * kTimelineStamps, stream_));
+    }
     jumps_ = alloc<uint32_t>((size_t)nbits_ * 800);
     const std::vector<uint32_t>& J = subsequence_jump_matrices(nbits_);
     SBMP_HIP(hipMemcpyAsync(jumps_, J.data(), (size_t)nbits_ * 800 * sizeof(uint32_t), hipMemcpyHostToDevice,
@@ -144,6 +153,11 @@ KgmtPlanner::~KgmtPlanner() {
 void KgmtPlanner::begin(const float* initial, const float* goal, const float* d_obstacles, int nObs, uint64_t seed) {
     if (!initial || !goal) throw Error(SBMP_ERR_INVALID_ARGUMENT, "initial/goal must be non-NULL");
     if (nObs < 0 || (nObs > 0 && !d_obstacles)) throw Error(SBMP_ERR_INVALID_ARGUMENT, "bad obstacles");
+    // D15: a non-finite root (x, y, theta, v) would only propagate NaN children; the
+    // kernels' min/max segment bounds rely on finite states (kgmt_device.h).
+    for (int i = 0; i < 4; ++i)
+        if (!std::isfinite(initial[i]))
+            throw Error(SBMP_ERR_INVALID_ARGUMENT, "initial state (x, y, theta, v) must be finite");
     SBMP_HIP(hipSetDevice(p_.device));
     KgmtDev& d = d_;
     hipStream_t s = stream_;
@@ -190,6 +204,7 @@ void KgmtPlanner::begin(const float* initial, const float* goal, const float* d_
     SBMP_HIP(hipGetLastError());
 
     t_next_ = 1;
+    lastFolded_ = 0;
     begun_ = true;
     wallMs_ = 0.0;
     SBMP_HIP(hipStreamSynchronize(s));
@@ -206,15 +221,34 @@ void KgmtPlanner::enqueue(int iterations) {
             enqueue_sharded_iteration(t);
             continue;
         }
-        launch_expand(d_, t, p_.agent, expandBlocks_, expandVariant_, expandChunks_, stream_, timing(K_EXPAND));
+        launch_expand(d_, t, p_.agent, expandBlocks_, expandVariant_, stream_, timing(K_EXPAND));
         launch_finish(d_, t, expandBlocks_, stream_, timing(K_FINISH));
+        if (t - lastFolded_ >= kFoldEvery) fold_to(t);
     }
     SBMP_HIP(hipGetLastError());
+}
+
+// Bring R2Valid / R2Invalid up to iteration tLast (k_fold_r2 over the key log).
+void KgmtPlanner::fold_to(int tLast) {
+    if (tLast <= lastFolded_) return;
+    if (d_.r2log) launch_fold_r2(d_, lastFolded_ + 1, tLast, stream_, timing(K_FOLD));
+    lastFolded_ = tLast;
 }
 
 void KgmtPlanner::sync() {
     SBMP_HIP(hipStreamSynchronize(stream_));
     wallMs_ = now_ms() - t0_;
+    if (d_.timeline && !timelineDumped_ && t_next_ > d_.timelineIter) {
+        const size_t n = (size_t)expandBlocks_ * (kBlock / kWave) * kTimelineStamps;
+        std::vector<long long> h(n);
+        SBMP_HIP(hipMemcpy(h.data(), d_.timeline, sizeof(long long) * n, hipMemcpyDeviceToHost));
+        const char* path = getenv("SBMP_TIMELINE_OUT");
+        if (FILE* f = fopen(path ? path : "sbmp_timeline.bin", "wb")) {
+            fwrite(h.data(), sizeof(long long), n, f);
+            fclose(f);
+        }
+        timelineDumped_ = true;
+    }
 }
 
 void KgmtPlanner::read_ctrl(std::vector<IterCtrl>& c, PlannerStatus& st) {
@@ -378,6 +412,7 @@ void KgmtPlanner::copy_flags(uint8_t* G, uint8_t* GNew) {
 
 void KgmtPlanner::copy_regions(int* R1, int* R1Avail, int* R1Valid, int* R1Invalid, float* R1Score, int* R2Avail,
                                int* R2Valid, int* R2Invalid) {
+    if (begun_) fold_to(t_next_ - 1);
     sync();
     std::vector<IterCtrl> c;
     PlannerStatus st;
@@ -493,7 +528,7 @@ void KgmtPlanner::collect_events() {
     pending_.clear();
 }
 
-static const char* kKernelNames[] = {"k_expand", "k_finish", "k_pack", "k_merge_insert"};
+static const char* kKernelNames[] = {"k_expand", "k_finish", "k_fold_r2", "k_pack", "k_merge_insert"};
 
 std::vector<float> KgmtPlanner::kernel_samples(const std::string& name) {
     collect_events();

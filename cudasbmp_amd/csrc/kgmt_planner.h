@@ -67,7 +67,7 @@ public:
     void enqueue_sharded_iteration(int t);
 
 private:
-    enum KernelId { K_EXPAND = 0, K_FINISH, K_PACK, K_MERGE, K_COUNT };
+    enum KernelId { K_EXPAND = 0, K_FINISH, K_FOLD, K_PACK, K_MERGE, K_COUNT };
     KernelTiming timing(int id);
     void collect_events();
     void read_ctrl(std::vector<IterCtrl>& c, PlannerStatus& st);
@@ -82,8 +82,10 @@ private:
     int t_next_ = 1;
     bool begun_ = false;
     int slotsPadded_ = 0, expandBlocks_ = 0, nbits_ = 1;
-    int expandVariant_ = 1;   // SBMP_EXPAND_VARIANT (obstacle-loop form, A/B knob)
-    int expandChunks_ = 1;    // SBMP_EXPAND_CHUNKS (256-slot blocks per expand workgroup)
+    int expandVariant_ = 0;   // SBMP_EXPAND_VARIANT: obstacle form, 0 = auto (3 if <= kMaxRegObs boxes, else 1)
+    bool timelineDumped_ = false;
+    int lastFolded_ = 0;      // iterations <= lastFolded_ are in R2Valid / R2Invalid
+    void fold_to(int tLast);
     uint32_t* jumps_ = nullptr;
     float4* obs_ = nullptr;
     int obsCap_ = 0;

@@ -25,7 +25,7 @@ def make(env, iters_total):
             key, val = kv.split("=")
             os.environ[key] = val
     k = KGMT(20.0, 20.0, 16, 8, iters_total, 1 << 24, 10, 1.0, 0.0, samplesPerIteration=262144,
-             batchRule="fill")
+             batchRule="fill", fixGNewClear=True)   # bench workload (bench.py --gnew-clear complete)
     return k
 
 
@@ -33,7 +33,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rounds", type=int, default=6)
     ap.add_argument("--iters", type=int, default=40)
-    ap.add_argument("--configs", default="SBMP_EXPAND_CHUNKS=1;SBMP_EXPAND_CHUNKS=2",
+    ap.add_argument("--configs", default="SBMP_EXPAND_VARIANT=1;SBMP_EXPAND_VARIANT=3",
                     help="';'-separated configurations, each a ','-separated list of ENV=value")
     a = ap.parse_args()
     obs = read_obstacles_csv(os.path.join(ROOT, "configurations", "obstacles", "obstacles.csv"))
@@ -56,6 +56,7 @@ def main():
             res[v].append((time.perf_counter() - t0) / a.iters * 1e6)
             if not prof_timed:
                 k.set_profiling(True)
+                k.enqueue_delay(4000.0)
                 k.enqueue(a.iters)
                 k.sync()
             st = k.kernel_stats()

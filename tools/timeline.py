@@ -1,0 +1,41 @@
+"""Phase timeline of one k_expand launch from s_memrealtime stamps (100 MHz).
+
+    SBMP_TIMELINE_ITER=40 SBMP_TIMELINE_OUT=gpurun_out/tl.bin python bench.py ...
+    python tools/timeline.py gpurun_out/tl.bin
+
+Stamps per wave (cudasbmp_amd/csrc/kgmt_kernels.hip, k_expand): 0 entry, 1 after the
+LDS prologue barrier, 2 after propagation, 3 after accept + slot stores, 4 after region
+aggregation, 5 after the flush barrier, 6 end of the counter flush.
+"""
+import sys
+
+import numpy as np
+
+NAMES = ["entry", "prologue", "propagate", "accept+store", "count_regions", "barrier", "flush"]
+
+
+def main():
+    a = np.fromfile(sys.argv[1], dtype=np.int64).reshape(-1, 8)
+    live = a[a[:, 6] != 0]
+    print(f"{len(a)} waves, {len(live)} ran the full path")
+    t0 = live[:, 0].min()
+    us = (live[:, :7] - t0) / 100.0
+    print("stamp              p0      p10     p50     p90     max   (us since first wave entry)")
+    for i, n in enumerate(NAMES):
+        q = np.percentile(us[:, i], [0, 10, 50, 90, 100])
+        print(f"  {i} {n:14s} " + " ".join(f"{x:7.2f}" for x in q))
+    print("phase durations per wave (us):  p10     p50     p90")
+    for i in range(1, 7):
+        dd = us[:, i] - us[:, i - 1]
+        q = np.percentile(dd, [10, 50, 90])
+        print(f"  {NAMES[i - 1]:>14s} -> {NAMES[i]:14s} " + " ".join(f"{x:7.2f}" for x in q))
+    blk = np.arange(len(a))[a[:, 6] != 0] // 4
+    for x in range(8):
+        m = (blk % 8) == x
+        if m.any():
+            print(f"  blockIdx%8=={x}: entry p50 {np.median(us[m, 0]):6.2f}  end p50 {np.median(us[m, 6]):6.2f}  "
+                  f"end max {us[m, 6].max():6.2f}")
+
+
+if __name__ == "__main__":
+    main()
