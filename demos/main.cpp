@@ -49,7 +49,7 @@ int main(int argc, char** argv) {
     int numObstacles = 0;
     SBMP_CHECK(sbmp_read_obstacles_csv(path, WORKSPACE_DIM, nullptr, 0, &numObstacles));
     std::vector<float> obstacles(2 * WORKSPACE_DIM * (size_t)numObstacles);
-    SBMP_CHECK(sbmp_read_obstacles_csv(path, WORKSPACE_DIM, obstacles.data(), numObstacles, &numObstacles));
+    SBMP_CHECK(sbmp_read_obstacles_csv(path, WORKSPACE_DIM, obstacles.data(), (int)obstacles.size(), &numObstacles));
     printf("Obstacles: \n");
     for (int i = 0; i < numObstacles; i++) {
         for (int j = 0; j < 2 * WORKSPACE_DIM; j++) printf("%f ", obstacles[i * 2 * WORKSPACE_DIM + j]);

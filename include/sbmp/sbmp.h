@@ -158,8 +158,9 @@ sbmp_status sbmp_kgmt_kernel_samples(sbmp_kgmt* h, const char* name, float* out,
 
 /* readObstaclesFromCSV (reference src/helper/helper.cu:11-34): whitespace or
  * comma separated floats, numObstacles = floats / (2*workspaceDim).  Returns
- * SBMP_ERR_IO instead of exit(1) when the file cannot be opened.  With
- * out == NULL only *numObstacles is computed. */
+ * SBMP_ERR_IO instead of exit(1) when the file cannot be opened.  capacity is
+ * the length of out in floats (>= 2*workspaceDim*numObstacles).  With out == NULL
+ * only *numObstacles is computed. */
 sbmp_status sbmp_read_obstacles_csv(const char* path, int workspaceDim, float* out, int capacity, int* numObstacles);
 
 /* Device memory helpers replacing demos/main.cu:60-61,64 (cudaMalloc/cudaMemcpy/cudaFree). */

@@ -113,7 +113,8 @@ def test_stepwise_bit_exact(d_obs, obstacles, oracle_lib):
     dict(maxTreeSize=700, numIterations=50),            # V2 branch, k < 32, tree-full termination (D13)
     dict(maxTreeSize=64, numIterations=50),             # tiny capacity: k = 0 path
     dict(n=4),                                          # different R2 sub-grid
-    dict(n=16, maxTreeSize=20000),
+    dict(n=16, maxTreeSize=20000),                      # > kLogMaxR2 cells: direct R2 atomics
+    dict(n=11, maxTreeSize=20000),                      # largest key-log grid (121 KB fold histogram)
     dict(numDisc=1),
     dict(numDisc=25, agentLength=2.5),
     dict(samplesPerIteration=8192, batchRule="fill", maxTreeSize=300000, numIterations=12, goalThreshold=0.0),
@@ -132,7 +133,8 @@ def test_configs_bit_exact(kw, d_obs, obstacles, oracle_lib):
 
 
 @pytest.mark.parametrize("case", ["no_obstacles", "root_outside", "root_in_obstacle_row", "many_obstacles",
-                                  "dense_obstacles_global_path", "goal_near_root"])
+                                  "dense_obstacles_global_path", "goal_near_root", "one_obstacle",
+                                  "eight_obstacles_registers", "nine_obstacles_lds"])
 def test_edge_cases_bit_exact(case, obstacles, oracle_lib):
     from cudasbmp_amd import DeviceBuffer
     init, goal, obs = list(DEMO_INITIAL), list(DEMO_GOAL), obstacles
@@ -151,6 +153,12 @@ def test_edge_cases_bit_exact(case, obstacles, oracle_lib):
         obs = np.concatenate([c - h, c + h], axis=1).astype(np.float32)
     elif case == "goal_near_root":
         goal[0], goal[1] = 5.2, 5.1
+    elif case == "one_obstacle":
+        obs = obstacles[4:5]
+    elif case in ("eight_obstacles_registers", "nine_obstacles_lds"):   # kMaxRegObs = 8
+        extra_boxes = np.array([[10, 12, 11, 13], [14, 3, 15, 4], [12, 15, 13, 16], [16, 10, 17, 11]],
+                               dtype=np.float32)
+        obs = np.concatenate([obstacles, extra_boxes[:3 if case.startswith("eight") else 4]])
     g, cfg, extra = _mk(numIterations=40)
     d = DeviceBuffer(obs) if len(obs) else None
     g.plan(init, goal, d, len(obs), seed=5)
