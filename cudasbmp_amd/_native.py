@@ -68,7 +68,7 @@ EXPORTED_SYMBOLS = (
     "sbmp_kgmt_copy_rng", "sbmp_kgmt_iter_log", "sbmp_kgmt_export_csv", "sbmp_kgmt_kernel_stats",
     "sbmp_kgmt_reset_kernel_stats", "sbmp_kgmt_set_profiling", "sbmp_kgmt_kernel_samples", "sbmp_kgmt_enqueue_delay",
     "sbmp_read_obstacles_csv", "sbmp_device_upload_f32", "sbmp_device_free",
-    "sbmp_device_count", "sbmp_comm_get_unique_id", "sbmp_kgmt_create_sharded",
+    "sbmp_device_count", "sbmp_comm_get_unique_id", "sbmp_kgmt_create_sharded", "sbmp_kgmt_create_local_group",
 )
 
 _lib = None
@@ -96,6 +96,7 @@ def lib():
         "sbmp_kgmt_default_params": [P(KgmtParams)],
         "sbmp_kgmt_create": [P(KgmtParams), P(vp)],
         "sbmp_kgmt_create_sharded": [P(KgmtParams), vp, i, i, P(vp)],
+        "sbmp_kgmt_create_local_group": [P(KgmtParams), i, P(vp)],
         "sbmp_comm_get_unique_id": [vp],
         "sbmp_kgmt_destroy": [vp],
         "sbmp_kgmt_plan": [vp, vp, vp, vp, i, ctypes.c_uint64, P(PlanResult)],

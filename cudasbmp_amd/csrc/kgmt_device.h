@@ -56,6 +56,7 @@ constexpr int kObsLds = 1;           // staged in LDS, rolled loop
 constexpr int kObsLds4 = 2;          // staged in LDS, 4-way batched reads
 constexpr int kObsReg = 16;          // kObsReg + n: exactly n <= kMaxRegObs boxes held in registers
 constexpr int kMaxRegObs = 8;
+constexpr int kMaxRanks = 8;         // ranks of one sharded planning problem (one node)
 constexpr int obs_in_registers(int obs) { return obs >= kObsReg ? obs - kObsReg : 0; }
 constexpr int kTimelineStamps = 8;   // s_memrealtime stamps per k_expand wave (diagnostics)
 constexpr int kFoldEvery = 16;       // iterations per R2 key-log fold (k_fold_r2)
@@ -76,9 +77,26 @@ struct KgmtDev {
     float4* uCtrl;
     uint4* rngA;
     uint2* rngB;
-    unsigned long long* gnew;
-    int* blockCount;      // GNew popcount per 256-slot block (written by k_expand)
-    int* blockOffsets;    // exclusive prefix of blockCount (written by k_plan)
+    // Per-iteration exchange, one fused u64 buffer per direction.
+    // *Out is what this rank produced, *In the sum over ranks (RCCL all-reduce, or
+    // the local group's sum kernel); on a single rank Out and In are the same memory.
+    // Every field is either disjoint per rank (GNew words and block counts of owned
+    // slots) or a carry-free counter (R1 deltas, R2New bytes), so a sum merges them.
+    unsigned long long* gnewOut;        // accept flags of owned slots (GNew), one bit per slot
+    unsigned long long* gnewIn;         // all ranks' flags (the insert kernels clear it, D6)
+    int* blockCountOut;                 // accepted (+ stale) children per owned 256-slot block
+    const int* blockCountIn;
+    unsigned long long* deltaOut;       // this iteration's valid (bits 0-31) / invalid (32-63) children per R1 cell
+    const unsigned long long* deltaIn;
+    uint8_t* r2newOut;                  // 1 = cell seen valid while unavailable in the snapshot
+    const uint8_t* r2newIn;
+    // Sharded ranks: accepted children packed in owned-slot order by k_pack into a
+    // record buffer [2 parities][recCap][state, ctrl]; the insert kernels of every
+    // rank read them from the owner's buffer (peer memory over xGMI).
+    int sharded;
+    int recCap;
+    float4* recOut;
+    const float4* recPeer[kMaxRanks];
     int* R1;
     int* R1Avail;
     int* R1Valid;
@@ -86,11 +104,9 @@ struct KgmtDev {
     int* R1Cov;           // available R2 cells per R1 cell (covR numerator, kept incrementally)
     uint32_t* R2Avail;    // live availability bits
     uint32_t* R2Snap;     // availability bits at the iteration start (D2)
-    uint32_t* R2New;      // cells seen valid this iteration while unavailable in the snapshot
     int* R2Valid;
     int* R2Invalid;
     float* R1Score;       // [2][nR1]
-    unsigned long long* delta;   // [nR1]: this iteration's valid (bits 0-31) / invalid (32-63) children per R1 cell
     uint16_t* r2log;      // [kFoldEvery][logSlots] per-child R2 keys (null when nR2 > kLogMaxR2)
     int logSlots;         // this rank's slots per log row
     const float4* obstacles;

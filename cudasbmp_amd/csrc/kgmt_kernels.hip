@@ -82,27 +82,50 @@ __device__ __forceinline__ int wave_sum(int v) {
     return v;
 }
 
-// Sum of counts[0, nb) and of counts[0, mine) over a 256-thread block.  counts is
-// allocated with a multiple-of-4 length and zero beyond every written entry.
+// Sum of counts[0, nb) and of counts[0, mine) over a 256-thread block, and of the
+// entries before `mine` whose index is owner mod nranks (the owner's earlier
+// blocks).  counts is allocated with a multiple-of-4 length and zero beyond every
+// written entry.
 __device__ __forceinline__ void block_prefix_total(const int* __restrict__ counts, int nb, int mine, int* pre,
-                                                   int* tot, int (*sRed)[kBlock / kWave]) {
-    int p = 0, s = 0;
+                                                   int* tot, int (*sRed)[kBlock / kWave], int nranks = 1,
+                                                   int owner = 0, int* preOwner = nullptr) {
+    int p = 0, s = 0, po = 0;
     const int nb4 = (nb + 3) & ~3;
     for (int i = threadIdx.x * 4; i < nb4; i += kBlock * 4) {
         const int4 v = *reinterpret_cast<const int4*>(counts + i);
+        const int e[4] = {v.x, v.y, v.z, v.w};
         s += v.x + v.y + v.z + v.w;
-        p += (i < mine ? v.x : 0) + (i + 1 < mine ? v.y : 0) + (i + 2 < mine ? v.z : 0) + (i + 3 < mine ? v.w : 0);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const bool before = i + k < mine;
+            p += before ? e[k] : 0;
+            po += (before && (i + k) % nranks == owner) ? e[k] : 0;
+        }
     }
     p = wave_sum(p);
     s = wave_sum(s);
+    po = wave_sum(po);
     const int wave = threadIdx.x >> 6;
     if ((threadIdx.x & (kWave - 1)) == 0) {
         sRed[0][wave] = p;
         sRed[1][wave] = s;
+        sRed[2][wave] = po;
     }
     __syncthreads();
     *pre = sRed[0][0] + sRed[0][1] + sRed[0][2] + sRed[0][3];
     *tot = sRed[1][0] + sRed[1][1] + sRed[1][2] + sRed[1][3];
+    if (preOwner) *preOwner = sRed[2][0] + sRed[2][1] + sRed[2][2] + sRed[2][3];
+}
+
+// A record of a peer rank (or of this device, same code): system-scope loads bypass
+// this GPU's caches, which may hold lines of the same parity buffer from two
+// iterations ago.
+__device__ __forceinline__ float4 load_record(const float4* p) {
+    unsigned long long* q = const_cast<unsigned long long*>(reinterpret_cast<const unsigned long long*>(p));
+    const unsigned long long a = __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    const unsigned long long b = __hip_atomic_load(q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    return make_float4(__uint_as_float((uint32_t)a), __uint_as_float((uint32_t)(a >> 32)),
+                       __uint_as_float((uint32_t)b), __uint_as_float((uint32_t)(b >> 32)));
 }
 
 // ------------------------------------------------------------------ expand
@@ -157,7 +180,7 @@ __global__ __launch_bounds__(kBlock) void k_expand(KgmtDev d, int t) {
     // the parent-row load follows it directly.
     const uint4 ra = d.rngA[slot];
     const uint2 rb = d.rngB[slot];
-    const unsigned long long oldWord = (lane == 0) ? d.gnew[slot >> 6] : 0ull;
+    const unsigned long long oldWord = (lane == 0) ? d.gnewIn[slot >> 6] : 0ull;
     const float scoreReg = (tid < d.nR1) ? d.R1Score[(t & 1) * d.nR1 + tid] : 0.0f;
     const float4 obsReg = (kLdsObs && tid < d.nObs) ? d.obstacles[tid] : make_float4(0.f, 0.f, 0.f, 0.f);
     uint32_t snapReg[kMaxR2Words / kBlock];
@@ -227,24 +250,29 @@ __global__ __launch_bounds__(kBlock) void k_expand(KgmtDev d, int t) {
         }
     }
     SBMP_STAMP(3);
-    // GNew |= accept (stale bits survive, D6).  A wave covers one 64-bit word.
+    // GNew |= accept (stale bits survive, D6).  A wave covers one 64-bit word; it is
+    // always written (a sharded rank's Out word must carry its stale bits too).
     const unsigned long long mask = __ballot(accept);
     if (lane == 0) {
         const unsigned long long now = oldWord | mask;
-        if (now != oldWord) d.gnew[slot >> 6] = now;
+        d.gnewOut[slot >> 6] = now;
         sWaveCnt[wave] = __popcll(now);   // slots past S: the stale bits' count
     }
     SBMP_STAMP(4);
     __syncthreads();
     SBMP_STAMP(5);
-    if (tid == 0) d.blockCount[gblock] = sWaveCnt[0] + sWaveCnt[1] + sWaveCnt[2] + sWaveCnt[3];
+    if (tid == 0) d.blockCountOut[gblock] = sWaveCnt[0] + sWaveCnt[1] + sWaveCnt[2] + sWaveCnt[3];
     for (int i = tid; i < d.nR1; i += kBlock) {   // one 64-bit atomic per touched cell
         const int v = sR1P[i];
-        if (v) atomicAdd(&d.delta[i], (unsigned long long)(v & 0xffff) | ((unsigned long long)(v >> 16) << 32));
+        if (v) atomicAdd(&d.deltaOut[i], (unsigned long long)(v & 0xffff) | ((unsigned long long)(v >> 16) << 32));
     }
-    for (int i = tid; i < nW; i += kBlock) {
-        const uint32_t w = sNew[i];
-        if (w) atomicOr(&d.R2New[i], w);
+    for (int i = tid; i < nW; i += kBlock) {   // R2New as one byte per cell (sums merge ranks)
+        uint32_t w = sNew[i];
+        while (w) {
+            const int b = __builtin_ctz(w);
+            w &= w - 1u;
+            d.r2newOut[32 * i + b] = 1;
+        }
     }
     SBMP_STAMP(6);
 #undef SBMP_STAMP
@@ -318,7 +346,7 @@ __device__ __forceinline__ void batch_rule(const KgmtDev& d, int treeSize, int n
 // Runs in block 0 of k_finish(t-1), concurrently with that launch's insert blocks
 // (it reads only what k_expand(t-1) wrote and nothing the insert blocks write).
 __device__ void plan_iteration(const KgmtDev& d, int t) {
-    __shared__ int sRed[2][kBlock / kWave];
+    __shared__ int sRed[3][kBlock / kWave];
     __shared__ int sCovInc[kMaxR1];
     __shared__ float sScore[kMaxR1];
     __shared__ float sPart[8];
@@ -335,20 +363,20 @@ __device__ void plan_iteration(const KgmtDev& d, int t) {
         pc = d.ctrl[t - 1];
         H = pc.H;
         int pre;
-        block_prefix_total(d.blockCount, (H + kBlock - 1) / kBlock, 0, &pre, &A, sRed);
+        block_prefix_total(d.blockCountIn, (H + kBlock - 1) / kBlock, 0, &pre, &A, sRed);
     }
     // Fold the previous expansion's region deltas into the tables and take the
     // availability snapshot for iteration t (t == 1: nothing to fold).
     for (int i = tid; i < kMaxR1; i += kBlock) sCovInc[i] = 0;
     for (int i = tid; i < d.nR1; i += kBlock) {
-        const unsigned long long dl = d.delta[i];
+        const unsigned long long dl = d.deltaIn[i];
         if (dl) {
             const int nv = (int)(dl & 0xffffffffull), ni = (int)(dl >> 32);
             d.R1[i] += nv + ni;            // every in-grid child (KGMT.cu:392)
             d.R1Valid[i] += nv;            // KGMT.cu:406
             d.R1Invalid[i] += ni;          // KGMT.cu:409
             if (nv) d.R1Avail[i] = 1;      // KGMT.cu:399-401
-            d.delta[i] = 0ull;
+            d.deltaOut[i] = 0ull;          // deltaIn == 0 implies every rank's deltaOut == 0
         }
     }
     __syncthreads();
@@ -356,9 +384,19 @@ __device__ void plan_iteration(const KgmtDev& d, int t) {
     const int nR2w = d.nR2 >> 5;
     for (int w = tid; w < nR2w; w += kBlock) {   // one thread owns one availability word
         uint32_t bits = d.R2Avail[w];
-        const uint32_t nw = d.R2New[w];
+        const uint4* nb = reinterpret_cast<const uint4*>(d.r2newIn + 32 * w);   // 32 cells, one byte each
+        const uint4 b0 = nb[0], b1 = nb[1];
+        const uint32_t q[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+        uint32_t nw = 0u;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {   // nonzero bytes -> 4 bits (byte sums <= nranks never carry)
+            const uint32_t hi = (((q[k] & 0x7f7f7f7fu) + 0x7f7f7f7fu) | q[k]) & 0x80808080u;
+            nw |= ((((hi >> 7) * 0x00204081u) >> 21) & 0xfu) << (4 * k);
+        }
         if (nw) {
-            d.R2New[w] = 0u;
+            uint4* ob = reinterpret_cast<uint4*>(d.r2newOut + 32 * w);
+            ob[0] = make_uint4(0u, 0u, 0u, 0u);
+            ob[1] = make_uint4(0u, 0u, 0u, 0u);
             uint32_t fresh = nw & ~bits;
             if (fresh) {
                 bits |= fresh;
@@ -451,21 +489,22 @@ __device__ void plan_iteration(const KgmtDev& d, int t) {
 // partial GNew clear (D6).  The block's j offset is the sum of the GNew counts of
 // the blocks before it (counts written by k_expand(t)).
 __device__ void insert_block(const KgmtDev& d, int t, int gblock) {
-    __shared__ int sRed[2][kBlock / kWave];
+    __shared__ int sRed[3][kBlock / kWave];
     __shared__ int sWaveCnt[kBlock / kWave];
     const int lane = threadIdx.x & (kWave - 1);
     const int wave = threadIdx.x >> 6;
     const int w = gblock * (kBlock / kWave) + wave;
     // Loads that do not depend on the control block go first (blockCount entries at
     // or past the high-water block were never written and are zero).
-    const unsigned long long word = d.gnew[w];
-    const int myCount = d.blockCount[gblock];
+    const unsigned long long word = d.gnewIn[w];
+    const int myCount = d.blockCountIn[gblock];
     const IterCtrl c = d.ctrl[t];
     if (!c.executed) return;
     if (gblock * kBlock >= c.H) return;
     if (myCount == 0) return;   // no accepted (or stale) slot: nothing to insert or clear
-    int pre, A;
-    block_prefix_total(d.blockCount, d.nBlocks, gblock, &pre, &A, sRed);
+    const int owner = gblock % d.nranks;   // block-cyclic slot ownership
+    int pre, A, preOwner;
+    block_prefix_total(d.blockCountIn, d.nBlocks, gblock, &pre, &A, sRed, d.nranks, owner, &preOwner);
 
     if (lane == 0) sWaveCnt[wave] = __popcll(word);
     __syncthreads();
@@ -481,8 +520,15 @@ __device__ void insert_block(const KgmtDev& d, int t, int gblock) {
         const int dst = c.treeSize + j;
         if (j < nIns && dst < d.M) {   // D13: the reference writes past M here
             const int slot = w * kWave + lane;
-            const float4 s = d.uState[slot];
-            const float4 u = d.uCtrl[slot];
+            float4 s, u;
+            if (!d.sharded) {
+                s = d.uState[slot];
+                u = d.uCtrl[slot];
+            } else {   // the owner packed its accepted slots in slot order (k_pack)
+                const float4* rec = d.recPeer[owner] + ((size_t)(t & 1) * d.recCap + preOwner + (j - pre)) * 2;
+                s = load_record(rec);
+                u = load_record(rec + 1);
+            }
             const int parent = __float_as_int(u.w);
             const float cost = d.treeCtrl[parent].w + u.z;   // getCost = duration (KGMT.cu:631-633)
             d.treeState[dst] = s;
@@ -499,7 +545,57 @@ __device__ void insert_block(const KgmtDev& d, int t, int gblock) {
         unsigned long long nw_ = word;
         if (base + kWave <= cleared) nw_ = 0ull;
         else if (base < cleared) nw_ = word & ~((1ull << (cleared - base)) - 1ull);
-        if (nw_ != word) d.gnew[w] = nw_;
+        if (nw_ != word) {
+            d.gnewIn[w] = nw_;
+            if (d.gnewOut != d.gnewIn && owner == d.rank) d.gnewOut[w] = nw_;   // the owner's own view
+        }
+    }
+}
+
+// Sharded ranks: this rank's accepted (and stale, D6) children of iteration t in
+// owned-slot order into record buffer t & 1, for the insert kernels of every rank.
+// A block's position is the count over this rank's earlier blocks (local counts).
+__global__ __launch_bounds__(kBlock) void k_pack(KgmtDev d, int t) {
+    __shared__ int sRed[3][kBlock / kWave];
+    __shared__ int sWaveCnt[kBlock / kWave];
+    const int lane = threadIdx.x & (kWave - 1);
+    const int wave = threadIdx.x >> 6;
+    const int lb = (int)blockIdx.x;
+    const int gblock = d.rank + d.nranks * lb;
+    const IterCtrl c = d.ctrl[t];
+    if (!c.executed || gblock * kBlock >= c.H) return;   // workgroup-uniform
+    const int w = gblock * (kBlock / kWave) + wave;
+    const unsigned long long word = d.gnewOut[w];
+    int pre = 0;
+    for (int i = threadIdx.x; i < lb; i += kBlock) pre += d.blockCountOut[d.rank + d.nranks * i];
+    pre = wave_sum(pre);
+    if (lane == 0) {
+        sRed[0][wave] = pre;
+        sWaveCnt[wave] = __popcll(word);
+    }
+    __syncthreads();
+    int off = sRed[0][0] + sRed[0][1] + sRed[0][2] + sRed[0][3];
+    for (int i = 0; i < wave; ++i) off += sWaveCnt[i];
+    if ((word >> lane) & 1ull) {
+        const int slot = w * kWave + lane;
+        float4* rec = d.recOut + ((size_t)(t & 1) * d.recCap + off + __popcll(word & ((1ull << lane) - 1ull))) * 2;
+        rec[0] = d.uState[slot];
+        rec[1] = d.uCtrl[slot];
+    }
+    __threadfence_system();   // peers read these over xGMI after the next all-reduce
+}
+
+// Local shard group (P ranks on one device, one stream): the all-reduce of the
+// exchange buffers as a sum kernel.
+struct XsumArgs {
+    const unsigned long long* send[kMaxRanks];
+    unsigned long long* recv[kMaxRanks];
+};
+__global__ void k_xsum(XsumArgs a, int nranks, long long n) {
+    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+        unsigned long long v = 0ull;
+        for (int q = 0; q < nranks; ++q) v += a.send[q][i];
+        for (int q = 0; q < nranks; ++q) a.recv[q][i] = v;
     }
 }
 
@@ -509,7 +605,7 @@ __global__ __launch_bounds__(kBlock) void k_finish(KgmtDev d, int t) {
         plan_iteration(d, t + 1);
         return;
     }
-    insert_block(d, t, d.rank + d.nranks * ((int)blockIdx.x - 1));
+    insert_block(d, t, (int)blockIdx.x - 1);   // every rank inserts every block (replicated tree)
 }
 
 // ------------------------------------------------------------------ init
@@ -660,6 +756,21 @@ void launch_fold_r2(const KgmtDev& d, int tFirst, int tLast, hipStream_t s, cons
 
 void launch_finish(const KgmtDev& d, int t, int insertBlocks, hipStream_t s, const KernelTiming& tm) {
     launch(k_finish, dim3(1 + insertBlocks), dim3(kBlock), 0, s, tm, d, t);
+}
+
+void launch_pack(const KgmtDev& d, int t, int blocks, hipStream_t s, const KernelTiming& tm) {
+    launch(k_pack, dim3(blocks), dim3(kBlock), 0, s, tm, d, t);
+}
+
+void launch_xsum(const unsigned long long* const* send, unsigned long long* const* recv, int nranks, long long n,
+                 hipStream_t s) {
+    XsumArgs a{};
+    for (int q = 0; q < nranks; ++q) {
+        a.send[q] = send[q];
+        a.recv[q] = recv[q];
+    }
+    const int blocks = (int)std::min<long long>((n + 255) / 256, 1024);
+    hipLaunchKernelGGL(k_xsum, dim3(blocks), dim3(256), 0, s, a, nranks, n);
 }
 
 void launch_fill_i32(int* p, int v, long long n, hipStream_t s) {

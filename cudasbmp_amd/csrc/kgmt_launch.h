@@ -23,10 +23,15 @@ void launch_expand(const KgmtDev& d, int t, int agent, int blocks, int variant, 
                    const KernelTiming& tm = KernelTiming());
 // k_fold_r2: add the key log of iterations [tFirst, tLast] (at most kFoldEvery) to R2Valid / R2Invalid.
 void launch_fold_r2(const KgmtDev& d, int tFirst, int tLast, hipStream_t s, const KernelTiming& tm = KernelTiming());
-// k_finish(t): insert iteration t (insertBlocks blocks) + prepare iteration t+1.
-// t = 0 prepares iteration 1 only (insertBlocks = 0).
+// k_finish(t): insert iteration t (insertBlocks = every global 256-slot block) +
+// prepare iteration t+1.  t = 0 prepares iteration 1 only (insertBlocks = 0).
 void launch_finish(const KgmtDev& d, int t, int insertBlocks, hipStream_t s,
                    const KernelTiming& tm = KernelTiming());
+// Sharded ranks: pack this rank's accepted children of iteration t (blocks = owned blocks).
+void launch_pack(const KgmtDev& d, int t, int blocks, hipStream_t s, const KernelTiming& tm = KernelTiming());
+// Local shard group: recv[q][i] = sum over ranks of send[r][i], for every rank q.
+void launch_xsum(const unsigned long long* const* send, unsigned long long* const* recv, int nranks, long long n,
+                 hipStream_t s);
 void launch_delay(double microseconds, hipStream_t s);
 void launch_fill_i32(int* p, int v, long long n, hipStream_t s);
 void launch_fill_f32(float* p, float v, long long n, hipStream_t s);

@@ -2,9 +2,10 @@
 //
 // Reference: KGMT::KGMT (src/planners/KGMT.cu:10-78) allocates ~25 thrust vectors;
 // KGMT::plan (KGMT.cu:80-317) runs a host loop with >= 6 blocking device->host
-// reads per iteration.  Here every iteration is three kernels whose sizes live
-// in device memory (IterCtrl), so the host only enqueues; it synchronises once
-// per `pollEvery` iterations to learn whether the loop has ended.
+// reads per iteration.  Here every iteration is two kernels (expand, finish; plus
+// pack + one all-reduce on a sharded rank) whose sizes live in device memory
+// (IterCtrl), so the host only enqueues; it synchronises once per `pollEvery`
+// iterations to learn whether the loop has ended.
 #include "kgmt_planner.h"
 
 #include <algorithm>
@@ -38,7 +39,8 @@ T* KgmtPlanner::alloc(size_t n) {
 
 static int round_up(long long x, long long m) { return (int)(((x + m - 1) / m) * m); }
 
-KgmtPlanner::KgmtPlanner(const sbmp_kgmt_params& p, int nranks, int rank, Exchange* ex) : p_(p), ex_(ex) {
+KgmtPlanner::KgmtPlanner(const sbmp_kgmt_params& p, int nranks, int rank, Exchange* ex, hipStream_t shared)
+    : p_(p), ex_(ex) {
     if (p.N * p.N != kMaxR1) throw Error(SBMP_ERR_INVALID_ARGUMENT, "N must be 16 (reference KGMT.cu:8 NUM_R1)");
     if (p.n < 1 || p.n > 16) throw Error(SBMP_ERR_INVALID_ARGUMENT, "n must be in [1, 16]");
     if (p.maxTreeSize < 1) throw Error(SBMP_ERR_INVALID_ARGUMENT, "maxTreeSize must be >= 1");
@@ -51,12 +53,18 @@ KgmtPlanner::KgmtPlanner(const sbmp_kgmt_params& p, int nranks, int rank, Exchan
         throw Error(SBMP_ERR_INVALID_ARGUMENT, "batchRule FILL needs samplesPerIteration > 0");
     if (p.agent != SBMP_AGENT_CAR && p.agent != SBMP_AGENT_POINT) throw Error(SBMP_ERR_INVALID_ARGUMENT, "unknown agent");
     if (!(p.width > 0.0f) || !(p.height > 0.0f)) throw Error(SBMP_ERR_INVALID_ARGUMENT, "width/height must be > 0");
-    if (nranks < 1 || rank < 0 || rank >= nranks) throw Error(SBMP_ERR_INVALID_ARGUMENT, "bad rank/nranks");
+    if (nranks < 1 || nranks > kMaxRanks || rank < 0 || rank >= nranks)
+        throw Error(SBMP_ERR_INVALID_ARGUMENT, "bad rank/nranks (at most 8 ranks)");
     int ndev = 0;
     SBMP_HIP(hipGetDeviceCount(&ndev));
     if (p.device < 0 || p.device >= ndev) throw Error(SBMP_ERR_INVALID_ARGUMENT, "no such HIP device");
     SBMP_HIP(hipSetDevice(p.device));
-    SBMP_HIP(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+    if (shared) {
+        stream_ = shared;
+        ownStream_ = false;
+    } else {
+        SBMP_HIP(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+    }
     if (const char* v = getenv("SBMP_EXPAND_VARIANT")) expandVariant_ = std::min(3, std::max(0, atoi(v)));
 
     const int M = p.maxTreeSize;
@@ -101,9 +109,6 @@ KgmtPlanner::KgmtPlanner(const sbmp_kgmt_params& p, int nranks, int rank, Exchan
     d.uCtrl = alloc<float4>(slotsPadded_);
     d.rngA = alloc<uint4>(slotsPadded_);
     d.rngB = alloc<uint2>(slotsPadded_);
-    d.gnew = alloc<unsigned long long>(nWords);
-    d.blockCount = alloc<int>(round_up(d.nBlocks, 4));   // read as int4
-    d.blockOffsets = alloc<int>(d.nBlocks);
     d.R1 = alloc<int>(d.nR1);
     d.R1Avail = alloc<int>(d.nR1);
     d.R1Valid = alloc<int>(d.nR1);
@@ -111,11 +116,38 @@ KgmtPlanner::KgmtPlanner(const sbmp_kgmt_params& p, int nranks, int rank, Exchan
     d.R1Cov = alloc<int>(d.nR1);
     d.R2Avail = alloc<uint32_t>(d.nR2 / 32);
     d.R2Snap = alloc<uint32_t>(d.nR2 / 32);
-    d.R2New = alloc<uint32_t>(d.nR2 / 32);
     d.R2Valid = alloc<int>(d.nR2);
     d.R2Invalid = alloc<int>(d.nR2);
     d.R1Score = alloc<float>(2 * d.nR1);
-    d.delta = alloc<unsigned long long>(d.nR1);
+    {   // exchange buffer: [R1 deltas | block counts (int4-readable) | GNew words | R2New bytes]
+        const size_t bcWords = round_up(d.nBlocks, 4) / 2, r2Words = round_up(d.nR2, 16) / 8;
+        xWords_ = (size_t)d.nR1 + bcWords + (size_t)nWords + r2Words;
+        xSend_ = alloc<unsigned long long>(xWords_);
+        xRecv_ = (nranks > 1 || ex) ? alloc<unsigned long long>(xWords_) : xSend_;
+        auto views = [&](unsigned long long* x, bool out) {
+            int* bc = reinterpret_cast<int*>(x + d.nR1);
+            unsigned long long* gn = x + d.nR1 + bcWords;
+            uint8_t* r2 = reinterpret_cast<uint8_t*>(gn + nWords);
+            if (out) {
+                d.deltaOut = x;
+                d.blockCountOut = bc;
+                d.gnewOut = gn;
+                d.r2newOut = r2;
+            } else {
+                d.deltaIn = x;
+                d.blockCountIn = bc;
+                d.gnewIn = gn;
+                d.r2newIn = r2;
+            }
+        };
+        views(xSend_, true);
+        views(xRecv_, false);
+    }
+    d.sharded = nranks > 1 || ex != nullptr;   // one RCCL rank still takes the sharded path
+    d.recCap = expandBlocks_ * kBlock;   // a rank never holds more flagged slots than it owns
+    d.recOut = d.sharded ? alloc<float4>((size_t)4 * d.recCap) : nullptr;
+    for (int q = 0; q < kMaxRanks; ++q) d.recPeer[q] = nullptr;
+    d.recPeer[rank] = d.recOut;
     d.logSlots = expandBlocks_ * kBlock;
     d.r2log = (d.nR2 <= kLogMaxR2) ? alloc<uint16_t>((size_t)kFoldEvery * d.logSlots) : nullptr;
     d.ctrl = alloc<IterCtrl>(p.numIterations + 2);
@@ -133,6 +165,11 @@ KgmtPlanner::KgmtPlanner(const sbmp_kgmt_params& p, int nranks, int rank, Exchan
     SBMP_HIP(hipMemcpyAsync(jumps_, J.data(), (size_t)nbits_ * 800 * sizeof(uint32_t), hipMemcpyHostToDevice,
                             stream_));
     SBMP_HIP(hipStreamSynchronize(stream_));
+    if (d.sharded && ex_) {   // map every rank's record buffer (IPC over xGMI)
+        void* peers[kMaxRanks] = {nullptr};
+        ex_->share_buffer(d.recOut, sizeof(float4) * 4 * (size_t)d.recCap, peers);
+        for (int q = 0; q < nranks; ++q) d.recPeer[q] = static_cast<const float4*>(peers[q]);
+    }
 }
 
 KgmtPlanner::~KgmtPlanner() {
@@ -147,7 +184,7 @@ KgmtPlanner::~KgmtPlanner() {
     for (hipEvent_t e : eventPool_) (void)hipEventDestroy(e);
     for (void* ptr : allocs_) (void)hipFree(ptr);
     if (obs_) (void)hipFree(obs_);
-    if (stream_) (void)hipStreamDestroy(stream_);
+    if (stream_ && ownStream_) (void)hipStreamDestroy(stream_);
 }
 
 void KgmtPlanner::begin(const float* initial, const float* goal, const float* d_obstacles, int nObs, uint64_t seed) {
@@ -165,10 +202,8 @@ void KgmtPlanner::begin(const float* initial, const float* goal, const float* d_
     SBMP_HIP(hipMemsetAsync(d.treeState, 0, sizeof(float4) * d.M, s));
     SBMP_HIP(hipMemsetAsync(d.treeCtrl, 0, sizeof(float4) * d.M, s));
     launch_fill_i32(d.treeParent, -1, d.M, s);
-    SBMP_HIP(hipMemsetAsync(d.gnew, 0, sizeof(unsigned long long) * d.nWords, s));
-    SBMP_HIP(hipMemsetAsync(d.blockCount, 0, sizeof(int) * round_up(d.nBlocks, 4), s));
-    SBMP_HIP(hipMemsetAsync(d.blockOffsets, 0, sizeof(int) * d.nBlocks, s));
-    SBMP_HIP(hipMemsetAsync(d.R2New, 0, sizeof(uint32_t) * (d.nR2 / 32), s));
+    SBMP_HIP(hipMemsetAsync(xSend_, 0, sizeof(unsigned long long) * xWords_, s));
+    if (xRecv_ != xSend_) SBMP_HIP(hipMemsetAsync(xRecv_, 0, sizeof(unsigned long long) * xWords_, s));
     for (int* a : {d.R1, d.R1Avail, d.R1Valid, d.R1Invalid, d.R1Cov})
         SBMP_HIP(hipMemsetAsync(a, 0, sizeof(int) * d.nR1, s));
     SBMP_HIP(hipMemsetAsync(d.R2Avail, 0, sizeof(uint32_t) * (d.nR2 / 32), s));
@@ -176,7 +211,6 @@ void KgmtPlanner::begin(const float* initial, const float* goal, const float* d_
     SBMP_HIP(hipMemsetAsync(d.R2Valid, 0, sizeof(int) * d.nR2, s));
     SBMP_HIP(hipMemsetAsync(d.R2Invalid, 0, sizeof(int) * d.nR2, s));
     launch_fill_f32(d.R1Score, 1.0f, 2 * d.nR1, s);
-    SBMP_HIP(hipMemsetAsync(d.delta, 0, sizeof(unsigned long long) * d.nR1, s));
     SBMP_HIP(hipMemsetAsync(d.ctrl, 0, sizeof(IterCtrl) * (p_.numIterations + 2), s));
 
     // Obstacles: a private float4 copy of the caller's device array (KGMT.cu:80 takes
@@ -215,17 +249,40 @@ void KgmtPlanner::begin(const float* initial, const float* goal, const float* d_
 
 void KgmtPlanner::enqueue(int iterations) {
     if (!begun_) throw Error(SBMP_ERR_STATE, "begin() has not been called");
-    for (int i = 0; i < iterations && t_next_ <= p_.numIterations; ++i) {
-        const int t = t_next_++;
-        if (d_.nranks > 1) {
-            enqueue_sharded_iteration(t);
-            continue;
+    if (d_.sharded && !ex_) throw Error(SBMP_ERR_STATE, "a local-group rank is driven by its group");
+    for (int i = 0; i < iterations; ++i) {
+        const int t = take_iteration();
+        if (t == 0) break;
+        stage_expand(t);
+        if (d_.sharded) {
+            stage_pack(t);
+            stage_exchange();
         }
-        launch_expand(d_, t, p_.agent, expandBlocks_, expandVariant_, stream_, timing(K_EXPAND));
-        launch_finish(d_, t, expandBlocks_, stream_, timing(K_FINISH));
-        if (t - lastFolded_ >= kFoldEvery) fold_to(t);
+        stage_finish(t);
+        stage_fold(t);
     }
     SBMP_HIP(hipGetLastError());
+}
+
+int KgmtPlanner::take_iteration() {
+    if (!begun_ || t_next_ > p_.numIterations) return 0;
+    return t_next_++;
+}
+
+void KgmtPlanner::stage_expand(int t) {
+    launch_expand(d_, t, p_.agent, expandBlocks_, expandVariant_, stream_, timing(K_EXPAND));
+}
+
+void KgmtPlanner::stage_pack(int t) { launch_pack(d_, t, expandBlocks_, stream_, timing(K_PACK)); }
+
+void KgmtPlanner::stage_exchange() {
+    if (ex_) ex_->allreduce_u64(xSend_, xRecv_, xWords_, stream_);
+}
+
+void KgmtPlanner::stage_finish(int t) { launch_finish(d_, t, d_.nBlocks, stream_, timing(K_FINISH)); }
+
+void KgmtPlanner::stage_fold(int t) {
+    if (t - lastFolded_ >= kFoldEvery) fold_to(t);
 }
 
 // Bring R2Valid / R2Invalid up to iteration tLast (k_fold_r2 over the key log).
@@ -280,7 +337,7 @@ bool KgmtPlanner::active() {
     return c.run && st.goalIdx == kNoGoal;
 }
 
-void KgmtPlanner::run(int pollEvery) {
+void Planner::run(int pollEvery) {
     if (pollEvery < 1) pollEvery = 1;
     while (true) {
         enqueue(pollEvery);
@@ -404,7 +461,7 @@ void KgmtPlanner::copy_flags(uint8_t* G, uint8_t* GNew) {
     }
     if (GNew) {
         std::vector<unsigned long long> w(d_.nWords);
-        SBMP_HIP(hipMemcpy(w.data(), d_.gnew, sizeof(unsigned long long) * d_.nWords, hipMemcpyDeviceToHost));
+        SBMP_HIP(hipMemcpy(w.data(), d_.gnewIn, sizeof(unsigned long long) * d_.nWords, hipMemcpyDeviceToHost));
         memset(GNew, 0, M);
         for (int s = 0; s < d_.nSlots; ++s) GNew[s] = (w[s >> 6] >> (s & 63)) & 1ull;
     }
@@ -427,8 +484,19 @@ void KgmtPlanner::copy_regions(int* R1, int* R1Avail, int* R1Valid, int* R1Inval
     cp(R1Valid, d_.R1Valid, sizeof(int) * n1);
     cp(R1Invalid, d_.R1Invalid, sizeof(int) * n1);
     cp(R1Score, d_.R1Score + (itr & 1) * n1, sizeof(float) * n1);
-    cp(R2Valid, d_.R2Valid, sizeof(int) * n2);
-    cp(R2Invalid, d_.R2Invalid, sizeof(int) * n2);
+    if (ex_ && (R2Valid || R2Invalid)) {   // sharded: each rank folded its own children
+        int* tmp = nullptr;
+        SBMP_HIP(hipMalloc(&tmp, sizeof(int) * 2 * n2));
+        ex_->allreduce_i32(d_.R2Valid, tmp, n2, stream_);
+        ex_->allreduce_i32(d_.R2Invalid, tmp + n2, n2, stream_);
+        SBMP_HIP(hipStreamSynchronize(stream_));
+        cp(R2Valid, tmp, sizeof(int) * n2);
+        cp(R2Invalid, tmp + n2, sizeof(int) * n2);
+        (void)hipFree(tmp);
+    } else {
+        cp(R2Valid, d_.R2Valid, sizeof(int) * n2);
+        cp(R2Invalid, d_.R2Invalid, sizeof(int) * n2);
+    }
     if (R2Avail) {
         std::vector<uint32_t> bits(n2 / 32);
         SBMP_HIP(hipMemcpy(bits.data(), d_.R2Avail, sizeof(uint32_t) * bits.size(), hipMemcpyDeviceToHost));
@@ -469,8 +537,16 @@ static void write_csv(const std::string& path, const T* v, size_t rows, size_t c
     }
 }
 
-void KgmtPlanner::export_csv(const std::string& dir) {
-    const size_t M = d_.M, n1 = d_.nR1, n2 = d_.nR2;
+void KgmtPlanner::copy_r2_partial(int* R2Valid, int* R2Invalid) {
+    if (begun_) fold_to(t_next_ - 1);
+    sync();
+    SBMP_HIP(hipMemcpy(R2Valid, d_.R2Valid, sizeof(int) * d_.nR2, hipMemcpyDeviceToHost));
+    SBMP_HIP(hipMemcpy(R2Invalid, d_.R2Invalid, sizeof(int) * d_.nR2, hipMemcpyDeviceToHost));
+}
+
+void Planner::export_csv(const std::string& dir) {
+    const sbmp_kgmt_params& p = params();
+    const size_t M = p.maxTreeSize, n1 = (size_t)p.N * p.N, n2 = n1 * p.n * p.n;
     mkdir(dir.c_str(), 0755);
     const std::string pre = dir.empty() ? "" : dir + "/";
     std::vector<float> samples(M * 7), costs(M), uS(M * 7), score(n1);
@@ -528,7 +604,7 @@ void KgmtPlanner::collect_events() {
     pending_.clear();
 }
 
-static const char* kKernelNames[] = {"k_expand", "k_finish", "k_fold_r2", "k_pack", "k_merge_insert"};
+static const char* kKernelNames[] = {"k_expand", "k_finish", "k_fold_r2", "k_pack"};
 
 std::vector<float> KgmtPlanner::kernel_samples(const std::string& name) {
     collect_events();

@@ -25,59 +25,116 @@ struct Error : std::runtime_error {
             throw ::sbmp::Error(SBMP_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(e_));      \
     } while (0)
 
-// Collective layer for the sharded planner (RCCL over xGMI, or an in-process
-// stand-in used by tests); see kgmt_sharded.cpp.
-class Exchange;
-
-class KgmtPlanner {
+// Collectives of one rank of a sharded planning problem (kgmt_sharded.cpp: RCCL
+// over xGMI, one process per GPU).
+class Exchange {
 public:
-    KgmtPlanner(const sbmp_kgmt_params& p, int nranks = 1, int rank = 0, Exchange* ex = nullptr);
-    ~KgmtPlanner();
+    virtual ~Exchange() = default;
+    // recv[i] = sum over ranks of send[i] (stream-ordered, also the per-iteration fence).
+    virtual void allreduce_u64(const unsigned long long* send, unsigned long long* recv, size_t n, hipStream_t s) = 0;
+    virtual void allreduce_i32(const int* send, int* recv, size_t n, hipStream_t s) = 0;
+    // Every rank's device buffer of the same size, mapped into this process (IPC).
+    virtual void share_buffer(void* own, size_t bytes, void* peers[kMaxRanks]) = 0;
+};
+
+// What the C ABI drives: one rank (single GPU or one rank of an RCCL group) or a
+// local shard group (several ranks on one GPU, used to test the sharded data flow).
+class Planner {
+public:
+    virtual ~Planner() = default;
+    virtual void begin(const float* initial, const float* goal, const float* d_obstacles, int nObs, uint64_t seed) = 0;
+    virtual void enqueue(int iterations) = 0;
+    virtual void sync() = 0;
+    virtual bool active() = 0;   // syncs; false once the loop has ended
+    virtual void result(sbmp_plan_result* r) = 0;
+    void run(int pollEvery);     // enqueue until the loop ends
+
+    virtual hipStream_t stream() const = 0;
+    virtual int num_slots() const = 0;
+    virtual const sbmp_kgmt_params& params() const = 0;
+
+    // exports (reference layouts)
+    virtual void copy_tree(float* samples, int* parent, float* costs) = 0;
+    virtual void copy_unexplored(float* samples, int* uParent) = 0;
+    virtual void copy_flags(uint8_t* G, uint8_t* GNew) = 0;
+    virtual void copy_regions(int* R1, int* R1Avail, int* R1Valid, int* R1Invalid, float* R1Score, int* R2Avail,
+                              int* R2Valid, int* R2Invalid) = 0;
+    virtual void copy_rng(uint32_t* states) = 0;
+    virtual std::vector<sbmp_iter_record> iter_log() = 0;
+    void export_csv(const std::string& dir);
+
+    virtual std::vector<sbmp_kernel_stat> kernel_stats() = 0;
+    virtual void reset_kernel_stats() = 0;
+    virtual void set_profiling(bool on) = 0;
+    virtual void enqueue_delay(double us) = 0;
+    virtual std::vector<float> kernel_samples(const std::string& name) = 0;
+};
+
+class KgmtPlanner : public Planner {
+public:
+    // nranks > 1: rank `rank` of a sharded problem.  ex = its RCCL collectives, or
+    // nullptr inside a LocalShardGroup (which then drives the stages itself);
+    // shared = a stream owned by the caller (the group), else the planner makes one.
+    KgmtPlanner(const sbmp_kgmt_params& p, int nranks = 1, int rank = 0, Exchange* ex = nullptr,
+                hipStream_t shared = nullptr);
+    ~KgmtPlanner() override;
     KgmtPlanner(const KgmtPlanner&) = delete;
     KgmtPlanner& operator=(const KgmtPlanner&) = delete;
 
-    void begin(const float* initial, const float* goal, const float* d_obstacles, int nObs, uint64_t seed);
-    void enqueue(int iterations);
-    void sync();
-    bool active();                    // syncs; false once the loop has ended
-    void result(sbmp_plan_result* r);
-    void run(int pollEvery);          // enqueue until the loop ends
+    void begin(const float* initial, const float* goal, const float* d_obstacles, int nObs, uint64_t seed) override;
+    void enqueue(int iterations) override;
+    void sync() override;
+    bool active() override;
+    void result(sbmp_plan_result* r) override;
 
-    hipStream_t stream() const { return stream_; }
-    int num_slots() const { return d_.nSlots; }
-    const sbmp_kgmt_params& params() const { return p_; }
+    hipStream_t stream() const override { return stream_; }
+    int num_slots() const override { return d_.nSlots; }
+    const sbmp_kgmt_params& params() const override { return p_; }
 
-    // exports (reference layouts)
-    void copy_tree(float* samples, int* parent, float* costs);
-    void copy_unexplored(float* samples, int* uParent);
-    void copy_flags(uint8_t* G, uint8_t* GNew);
+    void copy_tree(float* samples, int* parent, float* costs) override;
+    void copy_unexplored(float* samples, int* uParent) override;
+    void copy_flags(uint8_t* G, uint8_t* GNew) override;
     void copy_regions(int* R1, int* R1Avail, int* R1Valid, int* R1Invalid, float* R1Score, int* R2Avail,
-                      int* R2Valid, int* R2Invalid);
-    void copy_rng(uint32_t* states);
-    std::vector<sbmp_iter_record> iter_log();
-    void export_csv(const std::string& dir);
+                      int* R2Valid, int* R2Invalid) override;
+    void copy_rng(uint32_t* states) override;
+    std::vector<sbmp_iter_record> iter_log() override;
 
-    std::vector<sbmp_kernel_stat> kernel_stats();
-    void reset_kernel_stats();
-    void set_profiling(bool on) { p_.profileKernels = on ? 1 : 0; }
-    void enqueue_delay(double us) { launch_delay(us, stream_); }
-    std::vector<float> kernel_samples(const std::string& name);
+    std::vector<sbmp_kernel_stat> kernel_stats() override;
+    void reset_kernel_stats() override;
+    void set_profiling(bool on) override { p_.profileKernels = on ? 1 : 0; }
+    void enqueue_delay(double us) override { launch_delay(us, stream_); }
+    std::vector<float> kernel_samples(const std::string& name) override;
 
-    // sharded pieces (kgmt_sharded.cpp)
-    void enqueue_sharded_iteration(int t);
+    // ---- stages of one iteration (enqueue() composes them; a LocalShardGroup
+    // interleaves them across its ranks)
+    int take_iteration();                 // next iteration number, 0 past numIterations
+    void stage_expand(int t);
+    void stage_pack(int t);               // sharded ranks only
+    void stage_exchange();                // sharded ranks with an Exchange: the all-reduce
+    void stage_finish(int t);
+    void stage_fold(int t);               // every kFoldEvery iterations
+    unsigned long long* exchange_send() const { return xSend_; }
+    unsigned long long* exchange_recv() const { return xRecv_; }
+    size_t exchange_words() const { return xWords_; }
+    float4* record_buffer() const { return d_.recOut; }
+    void set_peer_records(int q, const float4* p) { d_.recPeer[q] = p; }
+    void copy_r2_partial(int* R2Valid, int* R2Invalid);   // this rank's folded R2 counters
+    int rank() const { return d_.rank; }
 
 private:
-    enum KernelId { K_EXPAND = 0, K_FINISH, K_FOLD, K_PACK, K_MERGE, K_COUNT };
+    enum KernelId { K_EXPAND = 0, K_FINISH, K_FOLD, K_PACK, K_COUNT };
     KernelTiming timing(int id);
     void collect_events();
     void read_ctrl(std::vector<IterCtrl>& c, PlannerStatus& st);
     int last_executed(const std::vector<IterCtrl>& c) const;
+    void fold_to(int tLast);
     template <typename T>
     T* alloc(size_t n);
 
     sbmp_kgmt_params p_;
     KgmtDev d_{};
     hipStream_t stream_ = nullptr;
+    bool ownStream_ = true;
     Exchange* ex_ = nullptr;
     int t_next_ = 1;
     bool begun_ = false;
@@ -85,7 +142,9 @@ private:
     int expandVariant_ = 0;   // SBMP_EXPAND_VARIANT: obstacle form, 0 = auto (3 if <= kMaxRegObs boxes, else 1)
     bool timelineDumped_ = false;
     int lastFolded_ = 0;      // iterations <= lastFolded_ are in R2Valid / R2Invalid
-    void fold_to(int tLast);
+    unsigned long long* xSend_ = nullptr;
+    unsigned long long* xRecv_ = nullptr;
+    size_t xWords_ = 0;
     uint32_t* jumps_ = nullptr;
     float4* obs_ = nullptr;
     int obsCap_ = 0;
@@ -102,8 +161,45 @@ private:
     long long launches_[K_COUNT] = {0};
     double totalMs_[K_COUNT] = {0};
     std::vector<float> samples_[K_COUNT];
+};
 
-    friend class ShardedDriver;
+// Several ranks of one sharded problem on ONE device and one stream, exchanging
+// through a sum kernel instead of RCCL and reading each other's record buffers
+// directly.  Same data flow as the RCCL ranks, so the GPU parity tests can prove
+// the sharded planner equal to the single-rank one on a one-GPU machine.
+class LocalShardGroup : public Planner {
+public:
+    LocalShardGroup(const sbmp_kgmt_params& p, int nranks);
+    ~LocalShardGroup() override;
+
+    void begin(const float* initial, const float* goal, const float* d_obstacles, int nObs, uint64_t seed) override;
+    void enqueue(int iterations) override;
+    void sync() override { r0().sync(); }
+    bool active() override { return r0().active(); }
+    void result(sbmp_plan_result* r) override { r0().result(r); }
+
+    hipStream_t stream() const override { return stream_; }
+    int num_slots() const override { return ranks_[0]->num_slots(); }
+    const sbmp_kgmt_params& params() const override { return ranks_[0]->params(); }
+
+    void copy_tree(float* samples, int* parent, float* costs) override { r0().copy_tree(samples, parent, costs); }
+    void copy_unexplored(float* samples, int* uParent) override;
+    void copy_flags(uint8_t* G, uint8_t* GNew) override { r0().copy_flags(G, GNew); }
+    void copy_regions(int* R1, int* R1Avail, int* R1Valid, int* R1Invalid, float* R1Score, int* R2Avail,
+                      int* R2Valid, int* R2Invalid) override;
+    void copy_rng(uint32_t* states) override;
+    std::vector<sbmp_iter_record> iter_log() override { return r0().iter_log(); }
+
+    std::vector<sbmp_kernel_stat> kernel_stats() override { return r0().kernel_stats(); }
+    void reset_kernel_stats() override;
+    void set_profiling(bool on) override;
+    void enqueue_delay(double us) override { r0().enqueue_delay(us); }
+    std::vector<float> kernel_samples(const std::string& name) override { return r0().kernel_samples(name); }
+
+private:
+    KgmtPlanner& r0() { return *ranks_[0]; }
+    hipStream_t stream_ = nullptr;
+    std::vector<KgmtPlanner*> ranks_;
 };
 
 double now_ms();

@@ -1,20 +1,201 @@
-// kgmt_sharded.cpp — multi-GPU sharding of one planning problem (placeholder;
-// the RCCL exchange lands in the next commit).
+// kgmt_sharded.cpp — one planning problem sharded over ranks.
+//
+// Slots are owned block-cyclically (256-slot block b -> rank b mod P); every rank
+// keeps a full replica of the tree, frontier and region tables.  Per iteration a
+// rank expands its own slots (k_expand), packs its accepted children in slot order
+// (k_pack), and all ranks all-reduce one fused exchange buffer (R1 deltas, block
+// counts, GNew words, R2New bytes; every field disjoint per rank or a carry-free
+// counter, so a sum merges them).  Then every rank inserts every block (k_finish),
+// reading other ranks' accepted children from their record buffers over xGMI.
+// The all-reduce is also the fence: rank q's record buffer of parity t & 1 is
+// rewritten only in iteration t + 2, after the all-reduce of t + 1, which waits
+// for every rank's inserts of t.
+//
+// RcclExchange: RCCL over xGMI, one process per GPU, record buffers mapped with
+// HIP IPC.  LocalShardGroup: P ranks on one GPU and one stream (a sum kernel for
+// the all-reduce, direct pointers for the records), so the sharded data flow can be
+// parity-tested against the single-rank planner on a one-GPU machine.
+#include <rccl/rccl.h>
+
+#include <cstring>
+
 #include "kgmt_planner.h"
 
 namespace sbmp {
 
-class Exchange {};
+#define SBMP_NCCL(expr)                                                                                  \
+    do {                                                                                                 \
+        ncclResult_t r_ = (expr);                                                                        \
+        if (r_ != ncclSuccess)                                                                           \
+            throw ::sbmp::Error(SBMP_ERR_COMM, std::string(#expr) + ": " + ncclGetErrorString(r_));     \
+    } while (0)
 
-void* sharded_create_comm(const uint8_t*, int, int, int) {
-    throw Error(SBMP_ERR_UNSUPPORTED, "sharded planner not built yet");
+static_assert(sizeof(ncclUniqueId) == SBMP_COMM_ID_BYTES, "RCCL unique id size");
+
+class RcclExchange : public Exchange {
+public:
+    RcclExchange(const uint8_t* id, int nranks, int rank, int device) : nranks_(nranks), rank_(rank) {
+        SBMP_HIP(hipSetDevice(device));
+        ncclUniqueId uid;
+        memcpy(&uid, id, sizeof(uid));
+        SBMP_NCCL(ncclCommInitRank(&comm_, nranks, uid, rank));
+        SBMP_HIP(hipStreamCreateWithFlags(&setup_, hipStreamNonBlocking));
+    }
+    ~RcclExchange() override {
+        for (void* p : mapped_) (void)hipIpcCloseMemHandle(p);
+        if (setup_) (void)hipStreamDestroy(setup_);
+        if (comm_) (void)ncclCommDestroy(comm_);
+    }
+
+    void allreduce_u64(const unsigned long long* send, unsigned long long* recv, size_t n, hipStream_t s) override {
+        SBMP_NCCL(ncclAllReduce(send, recv, n, ncclUint64, ncclSum, comm_, s));
+    }
+    void allreduce_i32(const int* send, int* recv, size_t n, hipStream_t s) override {
+        SBMP_NCCL(ncclAllReduce(send, recv, n, ncclInt32, ncclSum, comm_, s));
+    }
+    void share_buffer(void* own, size_t bytes, void* peers[kMaxRanks]) override {
+        (void)bytes;
+        hipIpcMemHandle_t h;
+        SBMP_HIP(hipIpcGetMemHandle(&h, own));
+        uint8_t* dev = nullptr;
+        SBMP_HIP(hipMalloc(&dev, sizeof(h) * (nranks_ + 1)));
+        SBMP_HIP(hipMemcpy(dev, &h, sizeof(h), hipMemcpyHostToDevice));
+        SBMP_NCCL(ncclAllGather(dev, dev + sizeof(h), sizeof(h), ncclUint8, comm_, setup_));
+        std::vector<hipIpcMemHandle_t> all(nranks_);
+        SBMP_HIP(hipStreamSynchronize(setup_));
+        SBMP_HIP(hipMemcpy(all.data(), dev + sizeof(h), sizeof(h) * nranks_, hipMemcpyDeviceToHost));
+        (void)hipFree(dev);
+        for (int q = 0; q < nranks_; ++q) {
+            if (q == rank_) {
+                peers[q] = own;
+                continue;
+            }
+            void* p = nullptr;
+            SBMP_HIP(hipIpcOpenMemHandle(&p, all[q], hipIpcMemLazyEnablePeerAccess));
+            mapped_.push_back(p);
+            peers[q] = p;
+        }
+    }
+
+private:
+    int nranks_, rank_;
+    ncclComm_t comm_ = nullptr;
+    hipStream_t setup_ = nullptr;
+    std::vector<void*> mapped_;
+};
+
+void* sharded_create_comm(const uint8_t* id, int nranks, int rank, int device) {
+    return new RcclExchange(id, nranks, rank, device);
 }
-void sharded_destroy_comm(void*) {}
-Exchange* sharded_exchange(void*) { return nullptr; }
-void comm_get_unique_id(uint8_t*) { throw Error(SBMP_ERR_UNSUPPORTED, "sharded planner not built yet"); }
+void sharded_destroy_comm(void* comm) { delete static_cast<RcclExchange*>(comm); }
+Exchange* sharded_exchange(void* comm) { return static_cast<RcclExchange*>(comm); }
 
-void KgmtPlanner::enqueue_sharded_iteration(int) {
-    throw Error(SBMP_ERR_UNSUPPORTED, "sharded planner not built yet");
+void comm_get_unique_id(uint8_t* id) {
+    ncclUniqueId uid;
+    SBMP_NCCL(ncclGetUniqueId(&uid));
+    memcpy(id, &uid, sizeof(uid));
+}
+
+// ---------------------------------------------------------------- local group
+LocalShardGroup::LocalShardGroup(const sbmp_kgmt_params& p, int nranks) {
+    if (nranks < 2 || nranks > kMaxRanks) throw Error(SBMP_ERR_INVALID_ARGUMENT, "local group needs 2..8 ranks");
+    SBMP_HIP(hipSetDevice(p.device));
+    SBMP_HIP(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+    try {
+        for (int r = 0; r < nranks; ++r) ranks_.push_back(new KgmtPlanner(p, nranks, r, nullptr, stream_));
+    } catch (...) {
+        for (KgmtPlanner* k : ranks_) delete k;
+        (void)hipStreamDestroy(stream_);
+        throw;
+    }
+    for (KgmtPlanner* k : ranks_)
+        for (KgmtPlanner* q : ranks_) k->set_peer_records(q->rank(), q->record_buffer());
+}
+
+LocalShardGroup::~LocalShardGroup() {
+    for (KgmtPlanner* k : ranks_) delete k;
+    if (stream_) (void)hipStreamDestroy(stream_);
+}
+
+void LocalShardGroup::begin(const float* initial, const float* goal, const float* d_obstacles, int nObs,
+                            uint64_t seed) {
+    for (KgmtPlanner* k : ranks_) k->begin(initial, goal, d_obstacles, nObs, seed);
+}
+
+void LocalShardGroup::enqueue(int iterations) {
+    const int P = (int)ranks_.size();
+    const unsigned long long* send[kMaxRanks];
+    unsigned long long* recv[kMaxRanks];
+    for (int q = 0; q < P; ++q) {
+        send[q] = ranks_[q]->exchange_send();
+        recv[q] = ranks_[q]->exchange_recv();
+    }
+    for (int i = 0; i < iterations; ++i) {
+        int t = 0;
+        for (KgmtPlanner* k : ranks_) t = k->take_iteration();   // all ranks advance together
+        if (t == 0) break;
+        for (KgmtPlanner* k : ranks_) k->stage_expand(t);
+        for (KgmtPlanner* k : ranks_) k->stage_pack(t);
+        launch_xsum(send, recv, P, (long long)ranks_[0]->exchange_words(), stream_);
+        for (KgmtPlanner* k : ranks_) k->stage_finish(t);
+        for (KgmtPlanner* k : ranks_) k->stage_fold(t);
+    }
+    SBMP_HIP(hipGetLastError());
+}
+
+// Slot rows live on their owning rank.
+void LocalShardGroup::copy_unexplored(float* samples, int* uParent) {
+    const int M = params().maxTreeSize, n = num_slots(), P = (int)ranks_.size();
+    std::vector<float> s((size_t)M * 7);
+    std::vector<int> u(M);
+    for (int q = 0; q < P; ++q) {
+        ranks_[q]->copy_unexplored(s.data(), u.data());
+        for (int i = 0; i < n; ++i) {
+            if ((i / kBlock) % P != q) continue;
+            if (samples) memcpy(samples + (size_t)i * 7, &s[(size_t)i * 7], sizeof(float) * 7);
+            if (uParent) uParent[i] = u[i];
+        }
+    }
+    for (int i = n; i < M; ++i) {
+        if (samples) memset(samples + (size_t)i * 7, 0, sizeof(float) * 7);
+        if (uParent) uParent[i] = -1;
+    }
+}
+
+void LocalShardGroup::copy_rng(uint32_t* states) {
+    const int n = num_slots(), P = (int)ranks_.size();
+    std::vector<uint32_t> st((size_t)n * 6);
+    for (int q = 0; q < P; ++q) {
+        ranks_[q]->copy_rng(st.data());
+        for (int i = 0; i < n; ++i)
+            if ((i / kBlock) % P == q) memcpy(states + (size_t)i * 6, &st[(size_t)i * 6], sizeof(uint32_t) * 6);
+    }
+}
+
+// R2Valid / R2Invalid: each rank folded the children of its own slots.
+void LocalShardGroup::copy_regions(int* R1, int* R1Avail, int* R1Valid, int* R1Invalid, float* R1Score, int* R2Avail,
+                                   int* R2Valid, int* R2Invalid) {
+    r0().copy_regions(R1, R1Avail, R1Valid, R1Invalid, R1Score, R2Avail, nullptr, nullptr);
+    if (!R2Valid && !R2Invalid) return;
+    const size_t n2 = (size_t)params().N * params().N * params().n * params().n;
+    std::vector<int> v(n2), iv(n2), sv(n2, 0), si(n2, 0);
+    for (KgmtPlanner* k : ranks_) {
+        k->copy_r2_partial(v.data(), iv.data());
+        for (size_t i = 0; i < n2; ++i) {
+            sv[i] += v[i];
+            si[i] += iv[i];
+        }
+    }
+    if (R2Valid) memcpy(R2Valid, sv.data(), sizeof(int) * n2);
+    if (R2Invalid) memcpy(R2Invalid, si.data(), sizeof(int) * n2);
+}
+
+void LocalShardGroup::reset_kernel_stats() {
+    for (KgmtPlanner* k : ranks_) k->reset_kernel_stats();
+}
+
+void LocalShardGroup::set_profiling(bool on) {
+    for (KgmtPlanner* k : ranks_) k->set_profiling(on);
 }
 
 }  // namespace sbmp

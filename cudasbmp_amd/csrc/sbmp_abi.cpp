@@ -12,9 +12,10 @@
 
 using sbmp::Error;
 using sbmp::KgmtPlanner;
+using sbmp::Planner;
 
 struct sbmp_kgmt {
-    KgmtPlanner* planner = nullptr;
+    Planner* planner = nullptr;
     void* comm = nullptr;   // sharded: owned collective context (kgmt_sharded.cpp)
 };
 
@@ -114,15 +115,27 @@ sbmp_status sbmp_kgmt_create_sharded(const sbmp_kgmt_params* p, const uint8_t id
         *out = nullptr;
         sbmp_kgmt* h = new sbmp_kgmt;
         try {
-            if (nranks > 1) {
-                h->comm = sbmp::sharded_create_comm(id, nranks, rank, p->device);
-                h->planner = new KgmtPlanner(*p, nranks, rank, sbmp::sharded_exchange(h->comm));
-            } else {
-                h->planner = new KgmtPlanner(*p);
-            }
+            h->comm = sbmp::sharded_create_comm(id, nranks, rank, p->device);
+            h->planner = new KgmtPlanner(*p, nranks, rank, sbmp::sharded_exchange(h->comm));
         } catch (...) {
             delete h->planner;
             if (h->comm) sbmp::sharded_destroy_comm(h->comm);
+            delete h;
+            throw;
+        }
+        *out = h;
+    });
+}
+
+sbmp_status sbmp_kgmt_create_local_group(const sbmp_kgmt_params* p, int nranks, sbmp_kgmt** out) {
+    return guarded([&] {
+        REQUIRE(p && out, "NULL argument");
+        *out = nullptr;
+        sbmp_kgmt* h = new sbmp_kgmt;
+        try {
+            h->planner = (nranks == 1) ? static_cast<Planner*>(new KgmtPlanner(*p))
+                                       : static_cast<Planner*>(new sbmp::LocalShardGroup(*p, nranks));
+        } catch (...) {
             delete h;
             throw;
         }
@@ -148,7 +161,7 @@ sbmp_status sbmp_kgmt_destroy(sbmp_kgmt* h) {
 
 #define PLANNER(h)                                                     \
     REQUIRE((h) && (h)->planner, "NULL planner handle");               \
-    KgmtPlanner& P = *(h)->planner
+    Planner& P = *(h)->planner
 
 sbmp_status sbmp_kgmt_begin(sbmp_kgmt* h, const float initial[7], const float goal[7], const float* d_obstacles,
                             int obstaclesCount, uint64_t seed) {

@@ -170,13 +170,19 @@ sbmp_status sbmp_device_count(int* count);
 
 /* ---- Multi-GPU: one planning problem sharded over ranks (one process per GPU) ----
  * Slots are owned block-cyclically (slot s -> rank (s/256) mod nranks); every
- * rank keeps a full replica of the tree; per iteration the ranks all-reduce
- * the region-counter deltas and all-gather the accepted children over RCCL,
- * so every rank builds the same tree as a 1-GPU run with the same seed. */
+ * rank keeps a full replica of the tree; per iteration the ranks all-reduce one
+ * fused exchange buffer over RCCL (region deltas, accept flags and counts) and
+ * read each other's accepted children over xGMI (IPC-mapped record buffers), so
+ * every rank builds the same tree as a 1-GPU run with the same seed. */
 #define SBMP_COMM_ID_BYTES 128
 sbmp_status sbmp_comm_get_unique_id(uint8_t id[SBMP_COMM_ID_BYTES]);
 sbmp_status sbmp_kgmt_create_sharded(const sbmp_kgmt_params* p, const uint8_t id[SBMP_COMM_ID_BYTES], int nranks,
                                      int rank, sbmp_kgmt** out);
+/* The same sharded data flow with nranks ranks on ONE device (p->device) and one
+ * stream: the all-reduce is a sum kernel, peer records are read directly.  For
+ * testing the sharding on a one-GPU machine; the handle behaves like one planner
+ * (exports merge the ranks).  nranks = 1 gives a plain planner. */
+sbmp_status sbmp_kgmt_create_local_group(const sbmp_kgmt_params* p, int nranks, sbmp_kgmt** out);
 
 #ifdef __cplusplus
 }

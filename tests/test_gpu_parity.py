@@ -214,3 +214,46 @@ def test_full_size_properties(fix_clear, d_obs, obstacles, oracle_lib):
     assert np.array_equal(reg["R1Valid"] + reg["R1Invalid"], reg["R1"])
     assert int(reg["R1"].sum()) <= r.samplesGenerated + 1
     assert np.all(reg["R2Avail"][reg["R2Valid"] > 0] == 1)
+
+
+@pytest.mark.parametrize("P,kw,seed", [
+    (2, dict(), 1),
+    (3, dict(), 2),
+    (4, dict(fixGNewClear=True), 3),
+    (2, dict(samplesPerIteration=4096, maxTreeSize=200000, numIterations=15, goalThreshold=0.0), 99),
+    (8, dict(samplesPerIteration=8192, batchRule="fill", maxTreeSize=300000, numIterations=12, goalThreshold=0.0), 7),
+    (3, dict(maxTreeSize=700, numIterations=50), 99),
+    (2, dict(agent="point", samplesPerIteration=2048, maxTreeSize=100000, numIterations=12, goalThreshold=0.0), 5),
+])
+def test_local_shard_group_bit_exact(P, kw, seed, d_obs, obstacles, oracle_lib):
+    """The sharded data flow (owned slots, k_pack records, summed exchange buffer,
+    every rank inserting every block) with P ranks on one GPU equals the oracle."""
+    from cudasbmp_amd import KGMT
+    cfg = dict(DEMO)
+    extra = {k: kw[k] for k in ("samplesPerIteration", "agent", "fixGNewClear", "batchRule") if k in kw}
+    cfg.update({k: v for k, v in kw.items() if k not in extra})
+    g = KGMT(**cfg, **extra, _local_group=P)
+    g.plan(DEMO_INITIAL, DEMO_GOAL, d_obs, len(obstacles), seed=seed)
+    o = _oracle(cfg, extra)
+    o.plan(DEMO_INITIAL, DEMO_GOAL, obstacles, seed)
+    assert_same_state(g, o, label=f"P={P} {kw}")
+
+
+def test_rccl_single_rank_sharded_path(d_obs, obstacles, oracle_lib):
+    """The RCCL rank path end to end on one GPU: ncclCommInitRank, the fused
+    ncclAllReduce per iteration, the IPC record-buffer exchange (own buffer) and
+    the R2 counter all-reduce at export, with k_pack / record reads in the loop."""
+    import ctypes
+    from cudasbmp_amd import KGMT
+    from cudasbmp_amd import _native as nat
+    uid = (ctypes.c_uint8 * nat.SBMP_COMM_ID_BYTES)()
+    nat.call("sbmp_comm_get_unique_id", uid)
+    kw = dict(samplesPerIteration=4096, batchRule="fill", maxTreeSize=200000, numIterations=20, goalThreshold=0.0)
+    cfg = dict(DEMO)
+    extra = {k: kw[k] for k in ("samplesPerIteration", "batchRule")}
+    cfg.update({k: v for k, v in kw.items() if k not in extra})
+    g = KGMT(**cfg, **extra, _sharded=(bytes(uid), 1, 0))
+    g.plan(DEMO_INITIAL, DEMO_GOAL, d_obs, len(obstacles), seed=21)
+    o = _oracle(cfg, extra)
+    o.plan(DEMO_INITIAL, DEMO_GOAL, obstacles, 21)
+    assert_same_state(g, o, label="rccl single rank")
