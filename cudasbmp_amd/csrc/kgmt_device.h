@@ -284,6 +284,43 @@ __device__ __forceinline__ void sincos_pred(float x, float* s, float* c) {
     }
 }
 
+// Wave-level culling of the per-step tests (register obstacle lists).  Every
+// segment box of a child lies inside the square of half-width R around its start
+// (sup |displacement| over the steps, plus a margin far above the rounding of the
+// update chain), so an obstacle no lane's square overlaps, under the same predicate,
+// can never be hit by the wave, and a wave whose squares all lie strictly inside
+// the workspace can never leave it.  Skipping those tests does not change a result.
+struct WaveCull {
+    unsigned boxes;    // bit i: some lane may overlap box i (wave-uniform)
+    bool bounds;       // some lane may leave the workspace (wave-uniform)
+};
+
+template <int OBS>
+__device__ __forceinline__ WaveCull wave_cull(float x0, float y0, float rx, float ry, const float4* obs,
+                                              const KgmtDev& d) {
+    WaveCull w;
+    rx = rx * 1.0001f + 1e-3f;
+    ry = ry * 1.0001f + 1e-3f;
+    const float minx = x0 - rx, maxx = x0 + rx, miny = y0 - ry, maxy = y0 + ry;
+    const bool inside = (minx > 0.0f) & (maxx < d.width) & (miny > 0.0f) & (maxy < d.height);
+    w.bounds = __ballot(!inside) != 0ull;
+    w.boxes = 0u;
+#pragma unroll
+    for (int i = 0; i < obs_in_registers(OBS); ++i)
+        if (__ballot(box_overlap(minx, miny, maxx, maxy, obs[i])) != 0ull) w.boxes |= 1u << i;
+    return w;
+}
+
+template <int OBS>
+__device__ __forceinline__ bool motion_valid_culled(float minx, float miny, float maxx, float maxy,
+                                                    const float4* __restrict__ obs, unsigned boxes) {
+    bool hit = false;
+#pragma unroll
+    for (int i = 0; i < obs_in_registers(OBS); ++i)
+        if ((boxes >> i) & 1u) hit |= box_overlap(minx, miny, maxx, maxy, obs[i]);   // uniform branch
+    return !hit;
+}
+
 // reference statePropagator.cu:5-76 (car).  Same operation sequence as the oracle
 // (D9-D11): fmaf where nvcc would contract, steering via one double fma.
 // v / agentLength: when agentLength is a power of two, v * (1/agentLength) is the
@@ -304,13 +341,19 @@ __device__ __forceinline__ bool propagate_car(float4 p, Xorwow& rs, const KgmtDe
     const float dt = duration / (float)d.numDisc;
     float x = p.x, y = p.y, theta = p.z, v = p.w;
     const float tan_steering = tanf_d(steering);
+    // |v| <= |v0| + |a| t, so the displacement stays below T |v0| + |a| T^2 / 2.
+    WaveCull cull{~0u, true};
+    if (OBS >= kObsReg) {
+        const float r = duration * __builtin_fabsf(p.w) + 0.5f * __builtin_fabsf(a) * duration * duration;
+        cull = wave_cull<OBS>(p.x, p.y, r, r, obs, d);
+    }
     bool alive = true;
     for (int i = 0; i < d.numDisc; ++i) {
         float st, ct;
         sincos_pred(theta, &st, &ct);
         const float nx = __builtin_fmaf(v * ct, dt, x);
         const float ny = __builtin_fmaf(v * st, dt, y);
-        const bool oob = (nx <= 0.0f) | (nx >= d.width) | (ny <= 0.0f) | (ny >= d.height);
+        const bool oob = cull.bounds && ((nx <= 0.0f) | (nx >= d.width) | (ny <= 0.0f) | (ny >= d.height));
         const float vl = (d.invAgentLength != 0.0f) ? v * d.invAgentLength : v / d.agentLength;
         const float nth = __builtin_fmaf(vl * tan_steering, dt, theta);
         const float nv = __builtin_fmaf(a, dt, v);
@@ -319,7 +362,8 @@ __device__ __forceinline__ bool propagate_car(float4 p, Xorwow& rs, const KgmtDe
         // non-finite root, and finite states stay finite.
         const float minx = seg_min(x, nx), maxx = seg_max(x, nx);
         const float miny = seg_min(y, ny), maxy = seg_max(y, ny);
-        const bool freeSeg = motion_valid<OBS>(minx, miny, maxx, maxy, obs, d.nObs);
+        const bool freeSeg = (OBS >= kObsReg) ? motion_valid_culled<OBS>(minx, miny, maxx, maxy, obs, cull.boxes)
+                                              : motion_valid<OBS>(minx, miny, maxx, maxy, obs, d.nObs);
         const bool adv = alive & !oob;
         x = alive ? nx : x;
         y = alive ? ny : y;
@@ -344,14 +388,18 @@ __device__ __forceinline__ bool propagate_point(float4 p, Xorwow& rs, const Kgmt
     const float duration = __builtin_fmaf(xorwow_uniform(rs), 1.0f, 0.05f);
     const float dt = duration / (float)d.numDisc;
     float x = p.x, y = p.y;
+    WaveCull cull{~0u, true};
+    if (OBS >= kObsReg)
+        cull = wave_cull<OBS>(p.x, p.y, duration * __builtin_fabsf(vx), duration * __builtin_fabsf(vy), obs, d);
     bool alive = true;
     for (int i = 0; i < d.numDisc; ++i) {
         const float nx = __builtin_fmaf(vx, dt, x);
         const float ny = __builtin_fmaf(vy, dt, y);
-        const bool oob = (nx <= 0.0f) | (nx >= d.width) | (ny <= 0.0f) | (ny >= d.height);
+        const bool oob = cull.bounds && ((nx <= 0.0f) | (nx >= d.width) | (ny <= 0.0f) | (ny >= d.height));
         const float minx = seg_min(x, nx), maxx = seg_max(x, nx);   // see propagate_car
         const float miny = seg_min(y, ny), maxy = seg_max(y, ny);
-        const bool freeSeg = motion_valid<OBS>(minx, miny, maxx, maxy, obs, d.nObs);
+        const bool freeSeg = (OBS >= kObsReg) ? motion_valid_culled<OBS>(minx, miny, maxx, maxy, obs, cull.boxes)
+                                              : motion_valid<OBS>(minx, miny, maxx, maxy, obs, d.nObs);
         x = alive ? nx : x;
         y = alive ? ny : y;
         alive = alive & !oob & freeSeg;

@@ -158,13 +158,14 @@ __global__ __launch_bounds__(kBlock) void k_expand(KgmtDev d, int t) {
     long long* const tl = (d.timeline && t == d.timelineIter)
                               ? d.timeline + ((size_t)blockIdx.x * (kBlock / kWave) + wave) * kTimelineStamps
                               : nullptr;
+    // Stamps stay in registers and are stored once at the exit: a store in the middle
+    // would add vmcnt waits of its own (and alias every later load).
+    long long stamp[kTimelineStamps] = {0, 0, 0, 0, 0, 0, 0, 0};
 #define SBMP_STAMP(i)                                                                  \
     do {                                                                               \
-        if (tl && lane == 0) tl[i] = (long long)__builtin_amdgcn_s_memrealtime();      \
+        if (tl) stamp[i] = (long long)__builtin_amdgcn_s_memrealtime();                \
     } while (0)
-    // Entry stamp kept in a register: a store here would make every later load a
-    // possible alias of it.
-    const long long entryStamp = tl ? (long long)__builtin_amdgcn_s_memrealtime() : 0;
+    SBMP_STAMP(0);
     constexpr bool kLdsObs = (OBS == kObsLds || OBS == kObsLds4);
     constexpr int kRegObs = obs_in_registers(OBS);
     float4 ro[kRegObs > 0 ? kRegObs : 1];   // register-resident obstacle list
@@ -215,7 +216,6 @@ __global__ __launch_bounds__(kBlock) void k_expand(KgmtDev d, int t) {
         for (int i = tid + kBlock; i < d.nObs; i += kBlock) sObs[i] = d.obstacles[i];
     }
     __syncthreads();
-    if (tl && lane == 0) tl[0] = entryStamp;
     SBMP_STAMP(1);
     const float4* obs = (kRegObs > 0) ? ro : kLdsObs ? sObs : d.obstacles;
 
@@ -275,6 +275,14 @@ __global__ __launch_bounds__(kBlock) void k_expand(KgmtDev d, int t) {
         }
     }
     SBMP_STAMP(6);
+    if (tl) {   // placement: XCC id << 32 | HW_ID (wave, SIMD, CU, SE fields)
+        unsigned hw, xcc;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+        stamp[7] = ((long long)xcc << 32) | hw;
+    }
+    if (tl && lane == 0)
+        for (int i = 0; i < kTimelineStamps; ++i) tl[i] = stamp[i];
 #undef SBMP_STAMP
 }
 

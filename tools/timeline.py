@@ -29,6 +29,21 @@ def main():
         dd = us[:, i] - us[:, i - 1]
         q = np.percentile(dd, [10, 50, 90])
         print(f"  {NAMES[i - 1]:>14s} -> {NAMES[i]:14s} " + " ".join(f"{x:7.2f}" for x in q))
+    hw = live[:, 7] & 0xffffffff
+    xcc = (live[:, 7] >> 32) & 0xf
+    simd = (hw >> 4) & 3
+    cu = (hw >> 8) & 0xf
+    se = (hw >> 13) & 7
+    key = ((xcc * 8 + se) * 16 + cu) * 4 + simd
+    ends = us[:, 6]
+    uk, inv = np.unique(key, return_inverse=True)
+    per_max = np.array([ends[inv == i].max() for i in range(len(uk))])
+    per_n = np.bincount(inv)
+    print(f"SIMDs used {len(uk)}, waves per SIMD: min {per_n.min()} median {np.median(per_n)} max {per_n.max()}")
+    print("last wave end per SIMD (us): p10 %.2f p50 %.2f p90 %.2f max %.2f" % tuple(np.percentile(per_max, [10, 50, 90, 100])))
+    for n_ in sorted(set(per_n.tolist())):
+        m = per_n == n_
+        print(f"  SIMDs with {n_} waves: {m.sum():4d}, last end p50 {np.median(per_max[m]):.2f} max {per_max[m].max():.2f}")
     blk = np.arange(len(a))[a[:, 6] != 0] // 4
     for x in range(8):
         m = (blk % 8) == x
