@@ -262,9 +262,12 @@ __global__ __launch_bounds__(kBlock) void k_expand(KgmtDev d, int t) {
     __syncthreads();
     SBMP_STAMP(5);
     if (tid == 0) d.blockCountOut[gblock] = sWaveCnt[0] + sWaveCnt[1] + sWaveCnt[2] + sWaveCnt[3];
-    for (int i = tid; i < d.nR1; i += kBlock) {   // one 64-bit atomic per touched cell
-        const int v = sR1P[i];
-        if (v) atomicAdd(&d.deltaOut[i], (unsigned long long)(v & 0xffff) | ((unsigned long long)(v >> 16) << 32));
+    {   // one 64-bit atomic per touched cell, into this workgroup's replica
+        unsigned long long* const rep = d.deltaOut + (size_t)(blockIdx.x % kDeltaReps) * d.nR1;
+        for (int i = tid; i < d.nR1; i += kBlock) {
+            const int v = sR1P[i];
+            if (v) atomicAdd(&rep[i], (unsigned long long)(v & 0xffff) | ((unsigned long long)(v >> 16) << 32));
+        }
     }
     for (int i = tid; i < nW; i += kBlock) {   // R2New as one byte per cell (sums merge ranks)
         uint32_t w = sNew[i];
@@ -377,14 +380,21 @@ __device__ void plan_iteration(const KgmtDev& d, int t) {
     // availability snapshot for iteration t (t == 1: nothing to fold).
     for (int i = tid; i < kMaxR1; i += kBlock) sCovInc[i] = 0;
     for (int i = tid; i < d.nR1; i += kBlock) {
-        const unsigned long long dl = d.deltaIn[i];
+        unsigned long long v[kDeltaReps];
+#pragma unroll
+        for (int r = 0; r < kDeltaReps; ++r) v[r] = d.deltaIn[(size_t)r * d.nR1 + i];
+        unsigned long long dl = 0ull;   // replicas: carry-free sums
+#pragma unroll
+        for (int r = 0; r < kDeltaReps; ++r) {
+            dl += v[r];
+            d.deltaOut[(size_t)r * d.nR1 + i] = 0ull;
+        }
         if (dl) {
             const int nv = (int)(dl & 0xffffffffull), ni = (int)(dl >> 32);
             d.R1[i] += nv + ni;            // every in-grid child (KGMT.cu:392)
             d.R1Valid[i] += nv;            // KGMT.cu:406
             d.R1Invalid[i] += ni;          // KGMT.cu:409
             if (nv) d.R1Avail[i] = 1;      // KGMT.cu:399-401
-            d.deltaOut[i] = 0ull;          // deltaIn == 0 implies every rank's deltaOut == 0
         }
     }
     __syncthreads();

@@ -119,14 +119,15 @@ KgmtPlanner::KgmtPlanner(const sbmp_kgmt_params& p, int nranks, int rank, Exchan
     d.R2Valid = alloc<int>(d.nR2);
     d.R2Invalid = alloc<int>(d.nR2);
     d.R1Score = alloc<float>(2 * d.nR1);
-    {   // exchange buffer: [R1 deltas | block counts (int4-readable) | GNew words | R2New bytes]
+    {   // exchange buffer: [R1 delta replicas | block counts (int4-readable) | GNew words | R2New bytes]
+        const size_t dWords = round_up((long long)kDeltaReps * d.nR1, 2);   // block counts stay 16-B aligned
         const size_t bcWords = round_up(d.nBlocks, 4) / 2, r2Words = round_up(d.nR2, 16) / 8;
-        xWords_ = (size_t)d.nR1 + bcWords + (size_t)nWords + r2Words;
+        xWords_ = dWords + bcWords + (size_t)nWords + r2Words;
         xSend_ = alloc<unsigned long long>(xWords_);
         xRecv_ = (nranks > 1 || ex) ? alloc<unsigned long long>(xWords_) : xSend_;
         auto views = [&](unsigned long long* x, bool out) {
-            int* bc = reinterpret_cast<int*>(x + d.nR1);
-            unsigned long long* gn = x + d.nR1 + bcWords;
+            int* bc = reinterpret_cast<int*>(x + dWords);
+            unsigned long long* gn = x + dWords + bcWords;
             uint8_t* r2 = reinterpret_cast<uint8_t*>(gn + nWords);
             if (out) {
                 d.deltaOut = x;
