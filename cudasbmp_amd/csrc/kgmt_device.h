@@ -120,6 +120,7 @@ struct KgmtDev {
     // Diagnostics (tools/timeline.py): when non-null, lane 0 of every k_expand wave of
     // iteration timelineIter stores s_memrealtime stamps at its phase boundaries.
     long long* timeline;
+    long long* timelineFin;   // k_finish(timelineIter): [1 + nBlocks][kTimelineStamps], wave 0 of each workgroup
     int timelineIter;
 };
 

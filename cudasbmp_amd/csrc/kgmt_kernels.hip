@@ -352,91 +352,145 @@ __device__ __forceinline__ void batch_rule(const KgmtDev& d, int treeSize, int n
     }
 }
 
+#define SBMP_FIN_STAMP(i)                                                    \
+    do {                                                                     \
+        if (st) st[i] = (long long)__builtin_amdgcn_s_memrealtime();         \
+    } while (0)
+
 // Close iteration t-1 (accepted count, region deltas) and prepare iteration t:
 // frontier range, batch, updateR1 (KGMT.cu:485-538), availability snapshot.
 // Runs in block 0 of k_finish(t-1), concurrently with that launch's insert blocks
 // (it reads only what k_expand(t-1) wrote and nothing the insert blocks write).
-__device__ void plan_iteration(const KgmtDev& d, int t) {
+// It is the critical path of k_finish, so every load (all of them independent:
+// one R1 cell and up to kMaxR2Words / kBlock availability words per thread) is
+// issued at entry and the tables are updated in registers: one memory round trip
+// instead of six.  Block counts at or past the high-water block are zero (H never
+// decreases), so the accepted count is the sum over all blocks.
+__device__ void plan_iteration(const KgmtDev& d, int t, long long* st) {
     __shared__ int sRed[3][kBlock / kWave];
     __shared__ int sCovInc[kMaxR1];
     __shared__ float sScore[kMaxR1];
     __shared__ float sPart[8];
+    constexpr int kW = kMaxR2Words / kBlock;
 
     const int tid = threadIdx.x;
-    const bool ranPrev = (t > 1) && d.ctrl[t - 1].executed;
+    const int cell = min(tid, d.nR1 - 1);   // nR1 <= kMaxR1 == kBlock: one R1 cell per thread
+    const bool own = tid < d.nR1;
+    const int nn = d.n * d.n;
+    const int nR2w = d.nR2 >> 5;
+    // ---- loads
+    const IterCtrl pc = d.ctrl[t > 1 ? t - 1 : 0];
+    int cnt = 0;
+    for (int i = tid * 4; i < d.nBlocks; i += kBlock * 4) {   // counts are int4-readable
+        const int4 v = *reinterpret_cast<const int4*>(d.blockCountIn + i);
+        cnt += v.x + v.y + v.z + v.w;
+    }
+    unsigned long long dv[kDeltaReps];
+#pragma unroll
+    for (int r = 0; r < kDeltaReps; ++r) dv[r] = d.deltaIn[(size_t)r * d.nR1 + cell];
+    int r1 = d.R1[cell], r1v = d.R1Valid[cell], r1i = d.R1Invalid[cell], r1a = d.R1Avail[cell], r1c = d.R1Cov[cell];
+    uint32_t bits[kW];
+    uint4 nb0[kW], nb1[kW];
+#pragma unroll
+    for (int j = 0; j < kW; ++j) {
+        const int w = min(tid + j * kBlock, nR2w - 1);
+        if (j * kBlock < nR2w) {   // uniform
+            bits[j] = d.R2Avail[w];
+            const uint4* nb = reinterpret_cast<const uint4*>(d.r2newIn + 32 * w);   // 32 cells, one byte each
+            nb0[j] = nb[0];
+            nb1[j] = nb[1];
+        }
+    }
+
+    const bool ranPrev = (t > 1) && pc.executed;
     if (t > 1 && !ranPrev) {
         if (tid == 0) d.ctrl[t].run = 0;
         return;
     }
-    int treeSize = 1, gLo = 0, H = 0, A = 0;
-    IterCtrl pc;
-    if (ranPrev) {
-        pc = d.ctrl[t - 1];
-        H = pc.H;
-        int pre;
-        block_prefix_total(d.blockCountIn, (H + kBlock - 1) / kBlock, 0, &pre, &A, sRed);
-    }
-    // Fold the previous expansion's region deltas into the tables and take the
-    // availability snapshot for iteration t (t == 1: nothing to fold).
-    for (int i = tid; i < kMaxR1; i += kBlock) sCovInc[i] = 0;
-    for (int i = tid; i < d.nR1; i += kBlock) {
-        unsigned long long v[kDeltaReps];
-#pragma unroll
-        for (int r = 0; r < kDeltaReps; ++r) v[r] = d.deltaIn[(size_t)r * d.nR1 + i];
-        unsigned long long dl = 0ull;   // replicas: carry-free sums
-#pragma unroll
-        for (int r = 0; r < kDeltaReps; ++r) {
-            dl += v[r];
-            d.deltaOut[(size_t)r * d.nR1 + i] = 0ull;
-        }
-        if (dl) {
-            const int nv = (int)(dl & 0xffffffffull), ni = (int)(dl >> 32);
-            d.R1[i] += nv + ni;            // every in-grid child (KGMT.cu:392)
-            d.R1Valid[i] += nv;            // KGMT.cu:406
-            d.R1Invalid[i] += ni;          // KGMT.cu:409
-            if (nv) d.R1Avail[i] = 1;      // KGMT.cu:399-401
-        }
+    sCovInc[tid] = 0;
+    int A = 0;
+    if (ranPrev) {   // accepted children of iteration t-1
+        const int wsum = wave_sum(cnt);
+        if ((tid & (kWave - 1)) == 0) sRed[0][tid >> 6] = wsum;
     }
     __syncthreads();
-    const int nn = d.n * d.n;
-    const int nR2w = d.nR2 >> 5;
-    for (int w = tid; w < nR2w; w += kBlock) {   // one thread owns one availability word
-        uint32_t bits = d.R2Avail[w];
-        const uint4* nb = reinterpret_cast<const uint4*>(d.r2newIn + 32 * w);   // 32 cells, one byte each
-        const uint4 b0 = nb[0], b1 = nb[1];
-        const uint32_t q[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
-        uint32_t nw = 0u;
+    if (ranPrev) A = sRed[0][0] + sRed[0][1] + sRed[0][2] + sRed[0][3];
+    SBMP_FIN_STAMP(1);
+
+    // ---- fold the previous expansion's region deltas (t == 1: all zero)
+    unsigned long long dl = 0ull;   // replicas: carry-free sums
 #pragma unroll
-        for (int k = 0; k < 8; ++k) {   // nonzero bytes -> 4 bits (byte sums <= nranks never carry)
-            const uint32_t hi = (((q[k] & 0x7f7f7f7fu) + 0x7f7f7f7fu) | q[k]) & 0x80808080u;
-            nw |= ((((hi >> 7) * 0x00204081u) >> 21) & 0xfu) << (4 * k);
-        }
-        if (nw) {
-            uint4* ob = reinterpret_cast<uint4*>(d.r2newOut + 32 * w);
-            ob[0] = make_uint4(0u, 0u, 0u, 0u);
-            ob[1] = make_uint4(0u, 0u, 0u, 0u);
-            uint32_t fresh = nw & ~bits;
-            if (fresh) {
-                bits |= fresh;
-                d.R2Avail[w] = bits;
+    for (int r = 0; r < kDeltaReps; ++r) dl += dv[r];
+    const int nv = (int)(dl & 0xffffffffull), ni = (int)(dl >> 32);
+    r1 += nv + ni;      // every in-grid child (KGMT.cu:392)
+    r1v += nv;          // KGMT.cu:406
+    r1i += ni;          // KGMT.cu:409
+    if (nv) r1a = 1;    // KGMT.cu:399-401
+    // ---- R2 availability: cells seen valid while unavailable (KGMT.cu:396-402).
+    // All words are decided before any is stored: a store ahead of a later word's
+    // loaded data would make that use wait for the store as well (vmcnt is in order).
+    uint32_t nws[kW];
+#pragma unroll
+    for (int j = 0; j < kW; ++j) {
+        const int w = tid + j * kBlock;
+        nws[j] = 0u;
+        if (j * kBlock < nR2w && w < nR2w) {
+            const uint32_t q[8] = {nb0[j].x, nb0[j].y, nb0[j].z, nb0[j].w, nb1[j].x, nb1[j].y, nb1[j].z, nb1[j].w};
+            uint32_t nw = 0u;
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {   // nonzero bytes -> 4 bits (byte sums <= nranks never carry)
+                const uint32_t hi = (((q[k] & 0x7f7f7f7fu) + 0x7f7f7f7fu) | q[k]) & 0x80808080u;
+                nw |= ((((hi >> 7) * 0x00204081u) >> 21) & 0xfu) << (4 * k);
+            }
+            nws[j] = nw;
+            uint32_t fresh = nw & ~bits[j];
+            if (fresh && nn % 32 == 0) {   // the 32 cells of a word lie in one R1 cell
+                atomicAdd(&sCovInc[(32 * w) / nn], __popc(fresh));
+            } else {
                 while (fresh) {
-                    const int b = __builtin_ctz(fresh);
+                    const int k = __builtin_ctz(fresh);
                     fresh &= fresh - 1u;
-                    atomicAdd(&sCovInc[(32 * w + b) / nn], 1);
+                    atomicAdd(&sCovInc[(32 * w + k) / nn], 1);
                 }
             }
         }
-        d.R2Snap[w] = bits;   // snapshot for the next expand (D2)
+    }
+#pragma unroll
+    for (int j = 0; j < kW; ++j) {
+        const int w = tid + j * kBlock;
+        if (j * kBlock < nR2w && w < nR2w) {
+            const uint32_t nw = nws[j], b = bits[j];
+            if (nw) {
+                uint4* ob = reinterpret_cast<uint4*>(d.r2newOut + 32 * w);
+                ob[0] = make_uint4(0u, 0u, 0u, 0u);
+                ob[1] = make_uint4(0u, 0u, 0u, 0u);
+                if (nw & ~b) d.R2Avail[w] = b | nw;
+            }
+            d.R2Snap[w] = b | nw;   // snapshot for the next expand (D2)
+        }
     }
     __syncthreads();
-    for (int i = tid; i < d.nR1; i += kBlock)
-        if (sCovInc[i]) d.R1Cov[i] += sCovInc[i];
+    r1c += sCovInc[cell];
+    if (own) {
+#pragma unroll
+        for (int r = 0; r < kDeltaReps; ++r) d.deltaOut[(size_t)r * d.nR1 + cell] = 0ull;
+        if (dl) {
+            d.R1[cell] = r1;
+            d.R1Valid[cell] = r1v;
+            d.R1Invalid[cell] = r1i;
+            d.R1Avail[cell] = r1a;
+        }
+        if (sCovInc[cell]) d.R1Cov[cell] = r1c;
+    }
+    SBMP_FIN_STAMP(2);
+
+    int treeSize = 1, gLo = 0, H = 0;
     if (ranPrev) {
+        H = pc.H;
         treeSize = pc.treeSize + A;   // KGMT.cu:249
         gLo = pc.gLo + pc.nExp;
         if (tid == 0) d.ctrl[t - 1].A = A;
     }
-
     const int run_t = (t <= d.numIterations) && (treeSize < d.M);   // KGMT.cu:118,255
     int nG = 0, k = 0, nExp = 0;
     if (run_t) {
@@ -446,21 +500,17 @@ __device__ void plan_iteration(const KgmtDev& d, int t) {
     const int S = k * nExp;
     const int buf = t & 1;
     if (run_t) {   // updateR1 for iteration t
-        __syncthreads();
-        for (int i = tid; i < d.nR1; i += kBlock) {
-            float s = 0.0f;
-            if (d.R1Avail[i] != 0) {
-                const int nValid = d.R1Valid[i];
-                const float covR = (float)d.R1Cov[i] / (float)nn;
-                const float freeVol = (0.01f + (float)nValid) / (0.01f + (float)nValid + (float)d.R1Invalid[i]);
-                const float fv2 = freeVol * freeVol;
-                const float fv4 = fv2 * fv2;
-                const double r = (double)d.R1[i];
-                const double den = (double)(1.0f + covR) * (1.0 + r * r);
-                s = (float)((double)fv4 / den);
-            }
-            sScore[i] = s;
+        float sc = 0.0f;
+        if (r1a != 0) {
+            const float covR = (float)r1c / (float)nn;
+            const float freeVol = (0.01f + (float)r1v) / (0.01f + (float)r1v + (float)r1i);
+            const float fv2 = freeVol * freeVol;
+            const float fv4 = fv2 * fv2;
+            const double r = (double)r1;
+            const double den = (double)(1.0f + covR) * (1.0 + r * r);
+            sc = (float)((double)fv4 / den);
         }
+        sScore[tid] = own ? sc : 0.0f;
         __syncthreads();
         if (tid < 8) {   // CUB BlockReduce order (D8): balanced tree per 32 group ...
             float tt[32];
@@ -481,9 +531,10 @@ __device__ void plan_iteration(const KgmtDev& d, int t) {
         }
         __syncthreads();
         const float total = sPart[0];
-        for (int i = tid; i < d.nR1; i += kBlock)
-            d.R1Score[buf * d.nR1 + i] = (d.R1Avail[i] == 0) ? 1.0f : sScore[i] / total;
+        SBMP_FIN_STAMP(3);
+        if (own) d.R1Score[buf * d.nR1 + cell] = (r1a == 0) ? 1.0f : sc / total;
     }
+    SBMP_FIN_STAMP(4);
     if (tid == 0) {
         IterCtrl c;
         c.run = run_t;
@@ -506,7 +557,7 @@ __device__ void plan_iteration(const KgmtDev& d, int t) {
 // becomes row treeSize + j (findInd + updateG, KGMT.cu:225-245,540-593), goal test,
 // partial GNew clear (D6).  The block's j offset is the sum of the GNew counts of
 // the blocks before it (counts written by k_expand(t)).
-__device__ void insert_block(const KgmtDev& d, int t, int gblock) {
+__device__ void insert_block(const KgmtDev& d, int t, int gblock, long long* st) {
     __shared__ int sRed[3][kBlock / kWave];
     __shared__ int sWaveCnt[kBlock / kWave];
     const int lane = threadIdx.x & (kWave - 1);
@@ -520,9 +571,11 @@ __device__ void insert_block(const KgmtDev& d, int t, int gblock) {
     if (!c.executed) return;
     if (gblock * kBlock >= c.H) return;
     if (myCount == 0) return;   // no accepted (or stale) slot: nothing to insert or clear
+    SBMP_FIN_STAMP(1);
     const int owner = gblock % d.nranks;   // block-cyclic slot ownership
     int pre, A, preOwner;
     block_prefix_total(d.blockCountIn, d.nBlocks, gblock, &pre, &A, sRed, d.nranks, owner, &preOwner);
+    SBMP_FIN_STAMP(2);
 
     if (lane == 0) sWaveCnt[wave] = __popcll(word);
     __syncthreads();
@@ -557,6 +610,7 @@ __device__ void insert_block(const KgmtDev& d, int t, int gblock) {
             if (__builtin_sqrtf(d2) < d.goalThreshold) atomicMin(&d.status->goalIdx, dst);
         }
     }
+    SBMP_FIN_STAMP(3);
     if (lane == 0) {   // D6: only GNew[0 .. 32*grid) is cleared
         const long long cleared = d.fixGNewClear ? (1ll << 62) : 32ll * grid;
         const long long base = (long long)w * kWave;
@@ -619,11 +673,17 @@ __global__ void k_xsum(XsumArgs a, int nranks, long long n) {
 
 // k_finish(t): block 0 prepares iteration t+1, blocks 1.. insert iteration t.
 __global__ __launch_bounds__(kBlock) void k_finish(KgmtDev d, int t) {
-    if (blockIdx.x == 0) {
-        plan_iteration(d, t + 1);
-        return;
+    // Diagnostics (tools/timeline.py --finish): stamps of wave 0, kept in registers.
+    const bool tl = d.timelineFin && t == d.timelineIter && threadIdx.x < kWave;
+    long long st[kTimelineStamps] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (tl) st[0] = (long long)__builtin_amdgcn_s_memrealtime();
+    if (blockIdx.x == 0) plan_iteration(d, t + 1, tl ? st : nullptr);
+    else insert_block(d, t, (int)blockIdx.x - 1, tl ? st : nullptr);   // every rank inserts every block
+    if (tl) {
+        st[7] = (long long)__builtin_amdgcn_s_memrealtime();
+        if (threadIdx.x == 0)
+            for (int i = 0; i < kTimelineStamps; ++i) d.timelineFin[(size_t)blockIdx.x * kTimelineStamps + i] = st[i];
     }
-    insert_block(d, t, (int)blockIdx.x - 1);   // every rank inserts every block (replicated tree)
 }
 
 // ------------------------------------------------------------------ init

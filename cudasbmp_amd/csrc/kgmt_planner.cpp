@@ -14,6 +14,7 @@
 #include <cstring>
 #include <fstream>
 #include <iomanip>
+#include <string>
 #include <sys/stat.h>
 
 #include "kgmt_launch.h"
@@ -154,12 +155,15 @@ KgmtPlanner::KgmtPlanner(const sbmp_kgmt_params& p, int nranks, int rank, Exchan
     d.ctrl = alloc<IterCtrl>(p.numIterations + 2);
     d.status = alloc<PlannerStatus>(1);
     d.timeline = nullptr;
+    d.timelineFin = nullptr;
     d.timelineIter = -1;
     if (const char* v = getenv("SBMP_TIMELINE_ITER")) {   // diagnostics: tools/timeline.py
         d.timelineIter = atoi(v);
-        d.timeline = alloc<long long>((size_t)expandBlocks_ * (kBlock / kWave) * kTimelineStamps);
-        SBMP_HIP(hipMemsetAsync(d.timeline, 0,
-                                sizeof(long long) * expandBlocks_ * (kBlock / kWave) * kTimelineStamps, stream_));
+        const size_t n = (size_t)expandBlocks_ * (kBlock / kWave) * kTimelineStamps;
+        const size_t nf = (size_t)(1 + d.nBlocks) * kTimelineStamps;
+        d.timeline = alloc<long long>(n + nf);
+        d.timelineFin = d.timeline + n;
+        SBMP_HIP(hipMemsetAsync(d.timeline, 0, sizeof(long long) * (n + nf), stream_));
     }
     jumps_ = alloc<uint32_t>((size_t)nbits_ * 800);
     const std::vector<uint32_t>& J = subsequence_jump_matrices(nbits_);
@@ -298,11 +302,16 @@ void KgmtPlanner::sync() {
     wallMs_ = now_ms() - t0_;
     if (d_.timeline && !timelineDumped_ && t_next_ > d_.timelineIter) {
         const size_t n = (size_t)expandBlocks_ * (kBlock / kWave) * kTimelineStamps;
-        std::vector<long long> h(n);
-        SBMP_HIP(hipMemcpy(h.data(), d_.timeline, sizeof(long long) * n, hipMemcpyDeviceToHost));
-        const char* path = getenv("SBMP_TIMELINE_OUT");
-        if (FILE* f = fopen(path ? path : "sbmp_timeline.bin", "wb")) {
+        const size_t nf = (size_t)(1 + d_.nBlocks) * kTimelineStamps;
+        std::vector<long long> h(n + nf);
+        SBMP_HIP(hipMemcpy(h.data(), d_.timeline, sizeof(long long) * (n + nf), hipMemcpyDeviceToHost));
+        const std::string path = getenv("SBMP_TIMELINE_OUT") ? getenv("SBMP_TIMELINE_OUT") : "sbmp_timeline.bin";
+        if (FILE* f = fopen(path.c_str(), "wb")) {
             fwrite(h.data(), sizeof(long long), n, f);
+            fclose(f);
+        }
+        if (FILE* f = fopen((path + ".fin").c_str(), "wb")) {   // k_finish stamps
+            fwrite(h.data() + n, sizeof(long long), nf, f);
             fclose(f);
         }
         timelineDumped_ = true;

@@ -2,6 +2,7 @@
 
     SBMP_TIMELINE_ITER=40 SBMP_TIMELINE_OUT=gpurun_out/tl.bin python bench.py ...
     python tools/timeline.py gpurun_out/tl.bin
+    python tools/timeline.py gpurun_out/tl.bin.fin      # k_finish of the same iteration
 
 Stamps per wave (cudasbmp_amd/csrc/kgmt_kernels.hip, k_expand): 0 entry, 1 after the
 LDS prologue barrier, 2 after propagation, 3 after accept + slot stores, 4 after region
@@ -14,7 +15,32 @@ import numpy as np
 NAMES = ["entry", "prologue", "propagate", "accept+store", "count_regions", "barrier", "flush"]
 
 
+FIN_PLAN = ["entry", "prefix", "deltas", "r2new", "cov", "scores", "R1Score", "end"]
+FIN_INSERT = ["entry", "loads", "prefix", "insert", "-", "-", "-", "end"]
+
+
+def finish(path):
+    """k_finish stamps (<out>.fin): block 0 = plan_iteration, blocks 1.. = insert_block."""
+    a = np.fromfile(path, dtype=np.int64).reshape(-1, 8)
+    t0 = a[a[:, 0] != 0, 0].min()
+    us = np.where(a != 0, (a - t0) / 100.0, np.nan)
+    print("plan_iteration (block 0): " + "  ".join(f"{n} {us[0, i]:.2f}" for i, n in enumerate(FIN_PLAN)
+                                                   if not np.isnan(us[0, i])))
+    ins = us[1:]
+    live = ~np.isnan(ins[:, 7])
+    print(f"insert blocks: {live.sum()} stamped")
+    print("stamp           p10     p50     p90     max")
+    for i, n in enumerate(FIN_INSERT):
+        col = ins[live, i]
+        col = col[~np.isnan(col)]
+        if len(col):
+            print(f"  {n:10s} " + " ".join(f"{x:7.2f}" for x in np.percentile(col, [10, 50, 90, 100])) + f"  (n={len(col)})")
+
+
 def main():
+    if sys.argv[1].endswith(".fin"):
+        finish(sys.argv[1])
+        return
     a = np.fromfile(sys.argv[1], dtype=np.int64).reshape(-1, 8)
     live = a[a[:, 6] != 0]
     print(f"{len(a)} waves, {len(live)} ran the full path")
