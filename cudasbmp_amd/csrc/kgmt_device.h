@@ -15,6 +15,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "sbmp/obstacle_grid.h"
 #include "sbmp/sbmp_math.h"
 
 #if defined(__clang__)
@@ -54,6 +55,7 @@ constexpr int kMaxLdsObs = 2048;     // obstacle lists up to 32 KB are staged in
 constexpr int kObsGlobal = 0;        // read from global memory, reference early exit (> kMaxLdsObs boxes)
 constexpr int kObsLds = 1;           // staged in LDS, rolled loop
 constexpr int kObsLds4 = 2;          // staged in LDS, 4-way batched reads
+constexpr int kObsGrid = 3;          // uniform-grid index (include/sbmp/obstacle_grid.h), large obstacle lists
 constexpr int kObsReg = 16;          // kObsReg + n: exactly n <= kMaxRegObs boxes held in registers
 constexpr int kMaxRegObs = 8;
 constexpr int kMaxRanks = 8;         // ranks of one sharded planning problem (one node)
@@ -115,6 +117,11 @@ struct KgmtDev {
     uint16_t* r2log;      // [kFoldEvery][logSlots] per-child R2 keys (null when nR2 > kLogMaxR2)
     int logSlots;         // this rank's slots per log row
     const float4* obstacles;
+    // Uniform-grid obstacle index (kObsGrid; null otherwise): gridG x gridG cells, CSR.
+    int gridG;
+    float gridInvW, gridInvH;
+    const int* gridStart;
+    const float4* gridBoxes;
     IterCtrl* ctrl;
     PlannerStatus* status;
     // Diagnostics (tools/timeline.py): when non-null, lane 0 of every k_expand wave of
@@ -368,8 +375,12 @@ __device__ __forceinline__ bool propagate_car(float4 p, Xorwow& rs, const KgmtDe
         // non-finite root, and finite states stay finite.
         const float minx = seg_min(x, nx), maxx = seg_max(x, nx);
         const float miny = seg_min(y, ny), maxy = seg_max(y, ny);
-        const bool freeSeg = (OBS >= kObsReg) ? motion_valid_culled<OBS>(minx, miny, maxx, maxy, obs, cull.boxes)
-                                              : motion_valid<OBS>(minx, miny, maxx, maxy, obs, d.nObs);
+        bool freeSeg;
+        if (OBS >= kObsReg) freeSeg = motion_valid_culled<OBS>(minx, miny, maxx, maxy, obs, cull.boxes);
+        else if (OBS == kObsGrid)   // only lanes whose result counts walk their cells
+            freeSeg = !(alive & !oob) || grid_motion_valid(minx, miny, maxx, maxy, d.gridG, d.gridInvW, d.gridInvH,
+                                                           d.gridStart, d.gridBoxes);
+        else freeSeg = motion_valid<OBS>(minx, miny, maxx, maxy, obs, d.nObs);
         const bool adv = alive & !oob;
         x = alive ? nx : x;
         y = alive ? ny : y;
@@ -404,8 +415,12 @@ __device__ __forceinline__ bool propagate_point(float4 p, Xorwow& rs, const Kgmt
         const bool oob = cull.bounds && ((nx <= 0.0f) | (nx >= d.width) | (ny <= 0.0f) | (ny >= d.height));
         const float minx = seg_min(x, nx), maxx = seg_max(x, nx);   // see propagate_car
         const float miny = seg_min(y, ny), maxy = seg_max(y, ny);
-        const bool freeSeg = (OBS >= kObsReg) ? motion_valid_culled<OBS>(minx, miny, maxx, maxy, obs, cull.boxes)
-                                              : motion_valid<OBS>(minx, miny, maxx, maxy, obs, d.nObs);
+        bool freeSeg;
+        if (OBS >= kObsReg) freeSeg = motion_valid_culled<OBS>(minx, miny, maxx, maxy, obs, cull.boxes);
+        else if (OBS == kObsGrid)
+            freeSeg = !(alive & !oob) || grid_motion_valid(minx, miny, maxx, maxy, d.gridG, d.gridInvW, d.gridInvH,
+                                                           d.gridStart, d.gridBoxes);
+        else freeSeg = motion_valid<OBS>(minx, miny, maxx, maxy, obs, d.nObs);
         x = alive ? nx : x;
         y = alive ? ny : y;
         alive = alive & !oob & freeSeg;

@@ -795,7 +795,9 @@ static void launch_expand_agent(const KgmtDev& d, int t, int blocks, int variant
                                 const KernelTiming& tm) {
     const size_t shm = sizeof(float4) * (size_t)d.nObs;
     const dim3 grid(blocks), block(kBlock);
-    if (d.nObs > kMaxLdsObs) {
+    if (d.gridStart) {   // the planner built the grid index (large lists, or variant 4)
+        launch(k_expand<AGENT, kObsGrid>, grid, block, 0, s, tm, d, t);
+    } else if (d.nObs > kMaxLdsObs) {
         launch(k_expand<AGENT, kObsGlobal>, grid, block, 0, s, tm, d, t);
     } else if (d.nObs <= kMaxRegObs && (variant == 0 || variant == 3)) {
         switch (d.nObs) {   // the box count is a compile-time constant of the register path

@@ -18,6 +18,7 @@
 #include <sys/stat.h>
 
 #include "kgmt_launch.h"
+#include "obstacle_grid.h"
 
 namespace sbmp {
 
@@ -66,7 +67,9 @@ KgmtPlanner::KgmtPlanner(const sbmp_kgmt_params& p, int nranks, int rank, Exchan
     } else {
         SBMP_HIP(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
     }
-    if (const char* v = getenv("SBMP_EXPAND_VARIANT")) expandVariant_ = std::min(3, std::max(0, atoi(v)));
+    // Obstacle-list form of k_expand (diagnostics / A-B): 0 auto, 1 LDS, 2 LDS x4,
+    // 3 registers, 4 grid index at any count, 5 global list without the grid.
+    if (const char* v = getenv("SBMP_EXPAND_VARIANT")) expandVariant_ = std::min(5, std::max(0, atoi(v)));
 
     const int M = p.maxTreeSize;
     const int nSlots = p.samplesPerIteration > 0 ? std::min(M, p.samplesPerIteration) : M;
@@ -189,6 +192,8 @@ KgmtPlanner::~KgmtPlanner() {
     for (hipEvent_t e : eventPool_) (void)hipEventDestroy(e);
     for (void* ptr : allocs_) (void)hipFree(ptr);
     if (obs_) (void)hipFree(obs_);
+    if (gridStart_) (void)hipFree(gridStart_);
+    if (gridBoxes_) (void)hipFree(gridBoxes_);
     if (stream_ && ownStream_) (void)hipStreamDestroy(stream_);
 }
 
@@ -230,6 +235,39 @@ void KgmtPlanner::begin(const float* initial, const float* goal, const float* d_
         SBMP_HIP(hipMemcpyAsync(obs_, d_obstacles, sizeof(float4) * nObs, hipMemcpyDeviceToDevice, s));
     d.obstacles = obs_;
     d.nObs = nObs;
+    // Large obstacle lists: the uniform-grid index (include/sbmp/obstacle_grid.h),
+    // built on the host from the caller's boxes; the global all-boxes loop remains
+    // as variant 5.
+    d.gridG = 0;
+    d.gridInvW = d.gridInvH = 0.0f;
+    d.gridStart = nullptr;
+    d.gridBoxes = nullptr;
+    if (nObs > 0 && ((nObs > kMaxLdsObs && expandVariant_ != 5) || expandVariant_ == 4)) {
+        std::vector<float> h((size_t)4 * nObs);
+        SBMP_HIP(hipMemcpy(h.data(), d_obstacles, sizeof(float) * h.size(), hipMemcpyDeviceToHost));
+        const HostObstacleGrid g = build_obstacle_grid(h.data(), nObs, d.width, d.height, 0);
+        const size_t nStart = g.start.size(), nBoxes = std::max<size_t>(1, g.boxes.size());
+        if (nStart > gridStartCap_) {
+            if (gridStart_) SBMP_HIP(hipFree(gridStart_));
+            gridStart_ = nullptr;
+            SBMP_HIP(hipMalloc(&gridStart_, sizeof(int) * nStart));
+            gridStartCap_ = nStart;
+        }
+        if (nBoxes > gridBoxesCap_) {
+            if (gridBoxes_) SBMP_HIP(hipFree(gridBoxes_));
+            gridBoxes_ = nullptr;
+            SBMP_HIP(hipMalloc(&gridBoxes_, sizeof(float4) * nBoxes));
+            gridBoxesCap_ = nBoxes;
+        }
+        SBMP_HIP(hipMemcpy(gridStart_, g.start.data(), sizeof(int) * nStart, hipMemcpyHostToDevice));
+        if (!g.boxes.empty())
+            SBMP_HIP(hipMemcpy(gridBoxes_, g.boxes.data(), sizeof(float4) * g.boxes.size(), hipMemcpyHostToDevice));
+        d.gridG = g.g;
+        d.gridInvW = g.invW;
+        d.gridInvH = g.invH;
+        d.gridStart = gridStart_;
+        d.gridBoxes = gridBoxes_;
+    }
     d.goalX = goal[0];
     d.goalY = goal[1];
 

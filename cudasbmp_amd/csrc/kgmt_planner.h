@@ -148,6 +148,10 @@ private:
     uint32_t* jumps_ = nullptr;
     float4* obs_ = nullptr;
     int obsCap_ = 0;
+    int* gridStart_ = nullptr;       // obstacle grid index (kObsGrid)
+    size_t gridStartCap_ = 0;
+    float4* gridBoxes_ = nullptr;
+    size_t gridBoxesCap_ = 0;
     std::vector<void*> allocs_;
     double wallMs_ = 0.0;
     double t0_ = 0.0;

@@ -8,6 +8,7 @@
 #include <vector>
 
 #include "kgmt_planner.h"
+#include "obstacle_grid.h"
 #include "sbmp/sbmp.h"
 
 using sbmp::Error;
@@ -356,6 +357,24 @@ sbmp_status sbmp_read_obstacles_csv(const char* path, int workspaceDim, float* o
             REQUIRE(capacity >= (int)v.size(), "capacity smaller than the file's float count");
             memcpy(out, v.data(), sizeof(float) * v.size());
         }
+    });
+}
+
+sbmp_status sbmp_obstacle_grid_query(const float* obstacles, int nObs, float width, float height, int gridSize,
+                                     const float* segments, int nSegments, uint8_t* freeOut, int* gridUsed) {
+    return guarded([&] {
+        REQUIRE(nObs >= 0 && nSegments >= 0 && (nObs == 0 || obstacles) && (nSegments == 0 || (segments && freeOut)),
+                "bad argument");
+        REQUIRE(width > 0.0f && height > 0.0f, "width and height must be positive");
+        const sbmp::HostObstacleGrid g = sbmp::build_obstacle_grid(obstacles, nObs, width, height, gridSize);
+        for (int i = 0; i < nSegments; ++i) {
+            const float* q = segments + 4 * i;
+            freeOut[i] = sbmp::grid_motion_valid(q[0], q[1], q[2], q[3], g.g, g.invW, g.invH, g.start.data(),
+                                                 g.boxes.data())
+                             ? 1
+                             : 0;
+        }
+        if (gridUsed) *gridUsed = g.g;
     });
 }
 

@@ -163,6 +163,15 @@ sbmp_status sbmp_kgmt_kernel_samples(sbmp_kgmt* h, const char* name, float* out,
  * only *numObstacles is computed. */
 sbmp_status sbmp_read_obstacles_csv(const char* path, int workspaceDim, float* out, int capacity, int* numObstacles);
 
+/* The uniform-grid obstacle index the planner uses for large obstacle lists
+ * (include/sbmp/obstacle_grid.h; replaces the all-boxes loop of isMotionValid,
+ * reference src/collisionCheck/collisionCheck.cu:16-28), evaluated on the host:
+ * freeOut[i] = isMotionValid(segment i) for nSegments boxes (minx, miny, maxx, maxy).
+ * gridSize <= 0 picks the planner's resolution; *gridUsed (optional) receives it.
+ * Host-only, no device needed (test entry point). */
+sbmp_status sbmp_obstacle_grid_query(const float* obstacles, int nObs, float width, float height, int gridSize,
+                                     const float* segments, int nSegments, uint8_t* freeOut, int* gridUsed);
+
 /* Device memory helpers replacing demos/main.cu:60-61,64 (cudaMalloc/cudaMemcpy/cudaFree). */
 sbmp_status sbmp_device_upload_f32(const float* host, size_t count, float** d_out);
 sbmp_status sbmp_device_free(void* d_ptr);

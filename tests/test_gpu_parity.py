@@ -257,3 +257,39 @@ def test_rccl_single_rank_sharded_path(d_obs, obstacles, oracle_lib):
     o = _oracle(cfg, extra)
     o.plan(DEMO_INITIAL, DEMO_GOAL, obstacles, 21)
     assert_same_state(g, o, label="rccl single rank")
+
+
+def _c5_obstacles():
+    import os
+    from conftest import ROOT
+    from cudasbmp_amd import read_obstacles_csv
+    return read_obstacles_csv(os.path.join(ROOT, "configurations", "obstacles", "obstacles_c5.csv"))
+
+
+@pytest.mark.parametrize("agent", ["car", "point"])
+@pytest.mark.parametrize("case,variant", [("demo_boxes_grid", "4"), ("random600_grid", "4"), ("c5_auto", "0"),
+                                          ("c5_global_list", "5")])
+def test_obstacle_grid_bit_exact(case, variant, agent, obstacles, oracle_lib, monkeypatch):
+    """The uniform-grid obstacle index (default above kMaxLdsObs boxes,
+    forced by SBMP_EXPAND_VARIANT=4) and the global all-boxes loop (variant 5) against
+    the oracle's isMotionValid loop (collisionCheck.cu:16-28)."""
+    from cudasbmp_amd import DeviceBuffer
+    monkeypatch.setenv("SBMP_EXPAND_VARIANT", variant)
+    if case == "demo_boxes_grid":
+        obs, kw = obstacles, dict(numIterations=40)
+    elif case == "random600_grid":
+        rng = np.random.default_rng(7)
+        c = rng.uniform(-1, 21, size=(600, 2)).astype(np.float32)
+        h = rng.uniform(0.02, 0.3, size=(600, 2)).astype(np.float32)
+        obs = np.concatenate([c - h, c + h], axis=1).astype(np.float32)
+        obs = obs[np.hypot(c[:, 0] - 5, c[:, 1] - 5) > 0.8]
+        kw = dict(numIterations=40)
+    else:   # the c5 field: 10,000 boxes, grid chosen automatically (or the global loop)
+        obs = _c5_obstacles()
+        kw = dict(numIterations=12, samplesPerIteration=8192, batchRule="fill", goalThreshold=0.0)
+    g, cfg, extra = _mk(agent=agent, **kw)
+    g.plan(DEMO_INITIAL, DEMO_GOAL, DeviceBuffer(obs), len(obs), seed=31)
+    o = _oracle(cfg, extra, threads=16)
+    o.plan(DEMO_INITIAL, DEMO_GOAL, obs, 31)
+    assert g.result().iterations > 3
+    assert_same_state(g, o, label=f"{case} {agent}")
