@@ -69,7 +69,7 @@ EXPORTED_SYMBOLS = (
     "sbmp_kgmt_reset_kernel_stats", "sbmp_kgmt_set_profiling", "sbmp_kgmt_kernel_samples", "sbmp_kgmt_enqueue_delay",
     "sbmp_read_obstacles_csv", "sbmp_device_upload_f32", "sbmp_device_free",
     "sbmp_device_count", "sbmp_comm_get_unique_id", "sbmp_kgmt_create_sharded", "sbmp_kgmt_create_local_group",
-    "sbmp_obstacle_grid_query",
+    "sbmp_obstacle_grid_query", "sbmp_kgmt_solution_path", "sbmp_random_tree",
 )
 
 _lib = None
@@ -122,6 +122,8 @@ def lib():
         "sbmp_kgmt_enqueue_delay": [vp, ctypes.c_double],
         "sbmp_read_obstacles_csv": [ctypes.c_char_p, i, vp, i, P(i)],
         "sbmp_obstacle_grid_query": [vp, i, ctypes.c_float, ctypes.c_float, i, vp, i, vp, P(i)],
+        "sbmp_kgmt_solution_path": [vp, i, vp, vp, vp, i, P(i)],
+        "sbmp_random_tree": [i, i, vp, i, i, i, vp, ctypes.c_longlong, P(ctypes.c_float)],
         "sbmp_device_upload_f32": [vp, ctypes.c_size_t, P(vp)],
         "sbmp_device_free": [vp],
         "sbmp_device_count": [P(i)],

@@ -174,6 +174,23 @@ SBMP_HD uint32_t xorwow_next(Xorwow& s) {
     return s.v4 + s.d;
 }
 
+// curand_init(seed, 0, 0): cuRAND's XORWOW seeding (_curand_init_scratch: salts
+// 0xaad26b49 / 0xf7dcefdd, multipliers 1099087573 / 2591861531), no skip-ahead.
+SBMP_HD Xorwow xorwow_seed(uint64_t seed) {
+    const uint32_t s0 = (uint32_t)seed ^ 0xaad26b49u;
+    const uint32_t s1 = (uint32_t)(seed >> 32) ^ 0xf7dcefddu;
+    const uint32_t t0 = 1099087573u * s0;
+    const uint32_t t1 = 2591861531u * s1;
+    Xorwow st;
+    st.d = 6615241u + t1 + t0;
+    st.v0 = 123456789u + t0;
+    st.v1 = 362436069u ^ t0;
+    st.v2 = 521288629u + t1;
+    st.v3 = 88675123u ^ t1;
+    st.v4 = 5783321u + t0;
+    return st;
+}
+
 // curand_uniform: x * 2^-32 + 2^-33 (product exact, one rounding).
 SBMP_HD float xorwow_uniform(Xorwow& s) {
     return (float)xorwow_next(s) * 2.3283064365386963e-10f + 1.1641532182693481e-10f;

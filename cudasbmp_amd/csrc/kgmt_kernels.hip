@@ -766,6 +766,33 @@ __global__ void k_export_tree(KgmtDev d, float* samples, float* costs) {
     }
 }
 
+// Solution path: rows root .. node by walking treeParent, root
+// first.  One thread; the depth is bounded by maxDepth (parent[j] < j, and every
+// iteration adds at most one level); out[0] = length, or -1 if the walk did not
+// reach the root within maxDepth rows.  rows/samples/costs hold maxDepth rows.
+__global__ void k_solution_path(KgmtDev d, int node, int maxDepth, int* out, int* rows, float* samples,
+                                float* costs) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    int depth = 0;
+    for (int j = node; j >= 0; j = d.treeParent[j]) {
+        if (++depth > maxDepth) {
+            out[0] = -1;
+            return;
+        }
+    }
+    out[0] = depth;
+    int k = depth - 1;
+    for (int j = node; j >= 0; j = d.treeParent[j], --k) {
+        const float4 st = d.treeState[j];
+        const float4 c = d.treeCtrl[j];
+        rows[k] = j;
+        float* o = samples + (size_t)k * 7;
+        o[0] = st.x; o[1] = st.y; o[2] = st.z; o[3] = st.w;
+        o[4] = c.x; o[5] = c.y; o[6] = c.z;
+        costs[k] = c.w;
+    }
+}
+
 __global__ void k_export_unexplored(KgmtDev d, float* samples, int* uParent) {
     for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < d.nSlots; i += gridDim.x * blockDim.x) {
         const float4 s = d.uState[i];
@@ -881,6 +908,11 @@ void launch_seed_root(const KgmtDev& d, float4 rs, float4 rc, int r1, int r2, hi
 
 void launch_export_tree(const KgmtDev& d, float* samples, float* costs, hipStream_t s) {
     hipLaunchKernelGGL(k_export_tree, dim3(1024), dim3(256), 0, s, d, samples, costs);
+}
+
+void launch_solution_path(const KgmtDev& d, int node, int maxDepth, int* out, int* rows, float* samples, float* costs,
+                          hipStream_t s) {
+    hipLaunchKernelGGL(k_solution_path, dim3(1), dim3(64), 0, s, d, node, maxDepth, out, rows, samples, costs);
 }
 
 void launch_export_unexplored(const KgmtDev& d, float* samples, int* uParent, hipStream_t s) {

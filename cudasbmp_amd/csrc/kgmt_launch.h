@@ -37,6 +37,8 @@ void launch_fill_i32(int* p, int v, long long n, hipStream_t s);
 void launch_fill_f32(float* p, float v, long long n, hipStream_t s);
 void launch_init_slots(const KgmtDev& d, const Xorwow& base, const uint32_t* jumps, int nbits, int blocks,
                        hipStream_t s);
+void launch_solution_path(const KgmtDev& d, int node, int maxDepth, int* out, int* rows, float* samples, float* costs,
+                          hipStream_t s);
 void launch_seed_root(const KgmtDev& d, float4 rs, float4 rc, int r1, int r2, hipStream_t s);
 void launch_export_tree(const KgmtDev& d, float* samples, float* costs, hipStream_t s);
 void launch_export_unexplored(const KgmtDev& d, float* samples, int* uParent, hipStream_t s);

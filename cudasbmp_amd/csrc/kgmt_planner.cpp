@@ -457,6 +457,39 @@ void KgmtPlanner::copy_tree(float* samples, int* parent, float* costs) {
     (void)hipFree(dC);
 }
 
+int KgmtPlanner::solution_path(int node, int* rows, float* samples, float* costs, int capacity) {
+    sbmp_plan_result r;
+    result(&r);   // syncs
+    if (node < 0) {
+        if (r.goalIndex < 0) return 0;
+        node = r.goalIndex;
+    }
+    const int rowsInTree = std::min(r.treeSize, d_.M);
+    if (node >= rowsInTree) throw Error(SBMP_ERR_INVALID_ARGUMENT, "node is not a tree row");
+    const int maxDepth = p_.numIterations + 2;   // one level per iteration, plus the root
+    int* dI = nullptr;
+    float* dF = nullptr;
+    SBMP_HIP(hipMalloc(&dI, sizeof(int) * (1 + (size_t)maxDepth)));
+    SBMP_HIP(hipMalloc(&dF, sizeof(float) * 8 * (size_t)maxDepth));
+    launch_solution_path(d_, node, maxDepth, dI, dI + 1, dF, dF + 7 * (size_t)maxDepth, stream_);
+    std::vector<int> hi(1 + (size_t)maxDepth);
+    std::vector<float> hf(8 * (size_t)maxDepth);
+    SBMP_HIP(hipMemcpyAsync(hi.data(), dI, sizeof(int) * hi.size(), hipMemcpyDeviceToHost, stream_));
+    SBMP_HIP(hipMemcpyAsync(hf.data(), dF, sizeof(float) * hf.size(), hipMemcpyDeviceToHost, stream_));
+    SBMP_HIP(hipStreamSynchronize(stream_));
+    (void)hipFree(dI);
+    (void)hipFree(dF);
+    const int len = hi[0];
+    if (len < 0) throw Error(SBMP_ERR_STATE, "parent chain longer than numIterations + 2 rows");
+    if ((rows || samples || costs) && capacity < len)
+        throw Error(SBMP_ERR_INVALID_ARGUMENT, "capacity " + std::to_string(capacity) + " < path length " +
+                                                   std::to_string(len));
+    if (rows) memcpy(rows, hi.data() + 1, sizeof(int) * len);
+    if (samples) memcpy(samples, hf.data(), sizeof(float) * 7 * len);
+    if (costs) memcpy(costs, hf.data() + 7 * (size_t)maxDepth, sizeof(float) * len);
+    return len;
+}
+
 void KgmtPlanner::copy_unexplored(float* samples, int* uParent) {
     sync();
     const size_t M = d_.M, n = d_.nSlots;

@@ -61,6 +61,9 @@ public:
                               int* R2Valid, int* R2Invalid) = 0;
     virtual void copy_rng(uint32_t* states) = 0;
     virtual std::vector<sbmp_iter_record> iter_log() = 0;
+    // Rows root .. node (node < 0: the solution node); returns the length (0: no
+    // solution).  Outputs may be null; capacity in rows (too small: SBMP_ERR_INVALID_ARGUMENT).
+    virtual int solution_path(int node, int* rows, float* samples, float* costs, int capacity) = 0;
     void export_csv(const std::string& dir);
 
     virtual std::vector<sbmp_kernel_stat> kernel_stats() = 0;
@@ -69,6 +72,11 @@ public:
     virtual void enqueue_delay(double us) = 0;
     virtual std::vector<float> kernel_samples(const std::string& name) = 0;
 };
+
+// Legacy random-tree generators (random_tree.hip): rows x (blocks * tpb) samples
+// of 7 floats into host memory.
+void random_tree(int device, int kind, const float* root, int rows, int blocks, int tpb, float* samples,
+                 float* kernelMs);
 
 class KgmtPlanner : public Planner {
 public:
@@ -98,6 +106,7 @@ public:
                       int* R2Valid, int* R2Invalid) override;
     void copy_rng(uint32_t* states) override;
     std::vector<sbmp_iter_record> iter_log() override;
+    int solution_path(int node, int* rows, float* samples, float* costs, int capacity) override;
 
     std::vector<sbmp_kernel_stat> kernel_stats() override;
     void reset_kernel_stats() override;
@@ -193,6 +202,9 @@ public:
                       int* R2Valid, int* R2Invalid) override;
     void copy_rng(uint32_t* states) override;
     std::vector<sbmp_iter_record> iter_log() override { return r0().iter_log(); }
+    int solution_path(int node, int* rows, float* samples, float* costs, int capacity) override {
+        return r0().solution_path(node, rows, samples, costs, capacity);   // every rank holds the whole tree
+    }
 
     std::vector<sbmp_kernel_stat> kernel_stats() override { return r0().kernel_stats(); }
     void reset_kernel_stats() override;

@@ -290,6 +290,19 @@ sbmp_status sbmp_kgmt_export_csv(sbmp_kgmt* h, const char* dir) {
     });
 }
 
+sbmp_status sbmp_kgmt_solution_path(sbmp_kgmt* h, int node, int* rows, float* samples, float* costs, int capacity,
+                                    int* length) {
+    return guarded([&] {
+        PLANNER(h);
+        REQUIRE(length, "length must be non-NULL");
+        const int len = P.solution_path(node, nullptr, nullptr, nullptr, 0);
+        *length = len;
+        if (!rows && !samples && !costs) return;
+        REQUIRE(capacity >= len, "capacity smaller than the path length");
+        P.solution_path(node, rows, samples, costs, capacity);
+    });
+}
+
 sbmp_status sbmp_kgmt_kernel_stats(sbmp_kgmt* h, sbmp_kernel_stat* out, int capacity, int* count) {
     return guarded([&] {
         PLANNER(h);
@@ -357,6 +370,26 @@ sbmp_status sbmp_read_obstacles_csv(const char* path, int workspaceDim, float* o
             REQUIRE(capacity >= (int)v.size(), "capacity smaller than the file's float count");
             memcpy(out, v.data(), sizeof(float) * v.size());
         }
+    });
+}
+
+sbmp_status sbmp_random_tree(int device, int kind, const float* root, int rows, int blocks, int threadsPerBlock,
+                             float* samples, long long capacity, float* kernelMs) {
+    return guarded([&] {
+        REQUIRE(root && samples, "root and samples must be non-NULL");
+        REQUIRE(kind == SBMP_RANDOM_TREE_NAIVE || kind == SBMP_RANDOM_TREE_COSTPROP, "unknown generator kind");
+        const bool naive = kind == SBMP_RANDOM_TREE_NAIVE;
+        if (rows <= 0) rows = naive ? 10 : 1;                       // NaivePlanner.cu:80 / CostPropPlanner.cu:87
+        if (blocks <= 0) blocks = naive ? 32 : 512;                 // :79 / :86
+        if (threadsPerBlock <= 0) threadsPerBlock = naive ? 32 : 1024;   // :78 / :85
+        REQUIRE(threadsPerBlock <= 1024, "threadsPerBlock must be <= 1024");
+        const long long n = (long long)rows * blocks * threadsPerBlock * 7;
+        REQUIRE(n < (1ll << 31), "tree larger than 2^31 floats (the reference indexes it with int)");
+        REQUIRE(capacity >= n, "capacity smaller than rows * blocks * threadsPerBlock * 7");
+        int ndev = 0;
+        SBMP_HIP(hipGetDeviceCount(&ndev));
+        REQUIRE(device >= 0 && device < ndev, "no such HIP device");
+        sbmp::random_tree(device, kind, root, rows, blocks, threadsPerBlock, samples, kernelMs);
     });
 }
 

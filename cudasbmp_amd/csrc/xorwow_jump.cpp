@@ -63,22 +63,7 @@ int g_nbits = 0;
 
 }  // namespace
 
-Xorwow curand_seed_state(uint64_t seed) {
-    // curand_init's seeding (_curand_init_scratch): salts 0xaad26b49 / 0xf7dcefdd,
-    // multipliers 1099087573 / 2591861531.
-    const uint32_t s0 = (uint32_t)seed ^ 0xaad26b49u;
-    const uint32_t s1 = (uint32_t)(seed >> 32) ^ 0xf7dcefddu;
-    const uint32_t t0 = 1099087573u * s0;
-    const uint32_t t1 = 2591861531u * s1;
-    Xorwow st;
-    st.d = 6615241u + t1 + t0;
-    st.v0 = 123456789u + t0;
-    st.v1 = 362436069u ^ t0;
-    st.v2 = 521288629u + t1;
-    st.v3 = 88675123u ^ t1;
-    st.v4 = 5783321u + t0;
-    return st;
-}
+Xorwow curand_seed_state(uint64_t seed) { return xorwow_seed(seed); }
 
 const std::vector<uint32_t>& subsequence_jump_matrices(int nbits) {
     std::lock_guard<std::mutex> lock(g_mu);

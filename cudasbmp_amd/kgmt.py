@@ -67,6 +67,25 @@ def device_ptr(obj) -> int:
     raise TypeError(f"cannot take a device pointer of {type(obj)!r}")
 
 
+def random_tree(kind: str, root, rows: int = 0, blocks: int = 0, threads_per_block: int = 0, device: int = 0):
+    """Legacy random-tree generators of the reference's Planner interface:
+    kind 'naive' (NaivePlanner.cu) or 'costprop' (CostPropPlanner.cu); sizes <= 0 take the
+    reference's.  Returns (samples (rows, blocks * threads_per_block, 7) float32, kernel ms)."""
+    naive = kind == "naive"
+    if kind not in ("naive", "costprop"):
+        raise ValueError("kind must be 'naive' or 'costprop'")
+    rows = rows if rows > 0 else (10 if naive else 1)
+    blocks = blocks if blocks > 0 else (32 if naive else 512)
+    tpb = threads_per_block if threads_per_block > 0 else (32 if naive else 1024)
+    r = np.zeros(7, dtype=np.float32)
+    r[: len(root)] = np.asarray(root, dtype=np.float32)[:7]
+    out = np.zeros((rows, blocks * tpb, 7), dtype=np.float32)
+    ms = ctypes.c_float()
+    nat.call("sbmp_random_tree", device, 0 if naive else 1, r.ctypes.data_as(ctypes.c_void_p), rows, blocks, tpb,
+             out.ctypes.data_as(ctypes.c_void_p), out.size, ctypes.byref(ms))
+    return out, ms.value
+
+
 def read_obstacles_csv(path: str, workspace_dim: int = 2) -> np.ndarray:
     """readObstaclesFromCSV (reference src/helper/helper.cu:11-34) through the ABI; (count, 4) float32."""
     n = ctypes.c_int()
@@ -208,6 +227,19 @@ class KGMT:
         nat.call("sbmp_kgmt_copy_tree", self._h, s.ctypes.data_as(ctypes.c_void_p),
                  p.ctypes.data_as(ctypes.c_void_p), c.ctypes.data_as(ctypes.c_void_p), M)
         return s, p, c
+
+    def solution_path(self, node: int = -1):
+        """Rows root .. node (default: the solution node) with their samples (n, 7) and
+        costs; empty arrays when there is no solution."""
+        n = ctypes.c_int()
+        nat.call("sbmp_kgmt_solution_path", self._h, int(node), None, None, None, 0, ctypes.byref(n))
+        rows = np.zeros(n.value, dtype=np.int32)
+        s = np.zeros((n.value, 7), dtype=np.float32)
+        c = np.zeros(n.value, dtype=np.float32)
+        if n.value:
+            nat.call("sbmp_kgmt_solution_path", self._h, int(node), rows.ctypes.data_as(ctypes.c_void_p),
+                     s.ctypes.data_as(ctypes.c_void_p), c.ctypes.data_as(ctypes.c_void_p), n.value, ctypes.byref(n))
+        return rows, s, c
 
     def unexplored(self):
         M = self.M

@@ -27,6 +27,7 @@
 #include <cstdlib>
 #include <ctime>
 #include <iostream>
+#include <vector>
 
 #include "sbmp/sbmp.h"
 
@@ -89,6 +90,15 @@ public:
     }
     void setWriteCsv(bool on) { writeCsv_ = on; }
     const sbmp_plan_result& result() const { return result_; }
+    // Path root .. solution node: tree rows and their 7-float
+    // samples; empty if plan() found no solution.
+    void solutionPath(std::vector<int>& rows, std::vector<float>& samples) const {
+        int n = 0;
+        SBMP_CHECK(sbmp_kgmt_solution_path(h_, -1, nullptr, nullptr, nullptr, 0, &n));
+        rows.assign(n, 0);
+        samples.assign(7 * (size_t)n, 0.0f);
+        if (n) SBMP_CHECK(sbmp_kgmt_solution_path(h_, -1, rows.data(), samples.data(), nullptr, n, &n));
+    }
     sbmp_kgmt* handle() const { return h_; }
 
     // Public fields of KGMT.cuh:33-43 that carry meaning outside the class.

@@ -146,6 +146,17 @@ sbmp_status sbmp_kgmt_iter_log(sbmp_kgmt* h, sbmp_iter_record* out, int capacity
 /* The 13 CSV dumps of KGMT.cu:299-311 (std::fixed, 10 decimals, helper.cuh:53-72) into dir. */
 sbmp_status sbmp_kgmt_export_csv(sbmp_kgmt* h, const char* dir);
 
+/* Solution path (the reference keeps only the goal node's cost,
+ * KGMT.cu:586-591): the tree rows from the root to `node` (node < 0: the
+ * solution node, result goalIndex), root first, found by walking treeParent.
+ * rows (ints), samples (7 floats per row, the samples.csv layout of
+ * KGMT.cu:299) and costs may each be NULL; capacity = their length in rows.
+ * *length = the path length (0 if node < 0 and there is no solution); with
+ * capacity < *length the call fails with SBMP_ERR_INVALID_ARGUMENT (and still sets
+ * *length), so a NULL/0 call returns the size to allocate. */
+sbmp_status sbmp_kgmt_solution_path(sbmp_kgmt* h, int node, int* rows, float* samples, float* costs, int capacity,
+                                    int* length);
+
 sbmp_status sbmp_kgmt_kernel_stats(sbmp_kgmt* h, sbmp_kernel_stat* out, int capacity, int* count);
 sbmp_status sbmp_kgmt_reset_kernel_stats(sbmp_kgmt* h);
 /* Turn per-launch HIP-event timing on/off for subsequently enqueued iterations. */
@@ -162,6 +173,20 @@ sbmp_status sbmp_kgmt_kernel_samples(sbmp_kgmt* h, const char* name, float* out,
  * the length of out in floats (>= 2*workspaceDim*numObstacles).  With out == NULL
  * only *numObstacles is computed. */
 sbmp_status sbmp_read_obstacles_csv(const char* path, int workspaceDim, float* out, int capacity, int* numObstacles);
+
+/* Legacy random-tree generators behind the reference's Planner interface
+ * (include/planners/Planner.cuh:6-12; the reference's CMake does not
+ * build them): SBMP_RANDOM_TREE_NAIVE = NaivePlanner::generateRandomTree
+ * (NaivePlanner.cu:76-140), SBMP_RANDOM_TREE_COSTPROP = CostPropPlanner
+ * (CostPropPlanner.cu:83-139).  rows / blocks / threadsPerBlock <= 0 take the
+ * reference's sizes (naive 10 x 32 x 32, costprop 1 x 512 x 1024).  samples: host
+ * array of capacity floats >= rows * blocks * threadsPerBlock * 7, row-major like the
+ * reference's tree; kernelMs (optional) receives the kernel time.  Semantics and the
+ * one deviation (D16): DESIGN.md. */
+#define SBMP_RANDOM_TREE_NAIVE 0
+#define SBMP_RANDOM_TREE_COSTPROP 1
+sbmp_status sbmp_random_tree(int device, int kind, const float* root, int rows, int blocks, int threadsPerBlock,
+                             float* samples, long long capacity, float* kernelMs);
 
 /* The uniform-grid obstacle index the planner uses for large obstacle lists
  * (include/sbmp/obstacle_grid.h; replaces the all-boxes loop of isMotionValid,

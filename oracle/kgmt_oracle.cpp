@@ -708,6 +708,51 @@ void oracle_replay(const oracle_params* prm, const float* obstacles, int nObs, c
     }
 }
 
+// Legacy random-tree generators (reference include/planners/Planner.cuh:6-12,
+// not built by the reference's CMake).  kind 0: NaivePlanner.cu:25-74 (curand_init(outIndex, 0, 0)
+// per sample); kind 1: CostPropPlanner.cu:25-81 (curand_init(gtid * rows, 0, 0) per thread).
+// 20 Euler steps of the car with a in [-2.5, 2.5), steering in [-pi/2, pi/2), duration in [0, 0.3).
+// D16: row r > 0 of a block grows from the block's first sample of row r - 1, the intent of
+// both kernels (NaivePlanner.cu:71 reads it from `root`, out of bounds; CostPropPlanner.cu:78
+// from the tree).  Contractions as D10/D11: x = fmaf(v*cos, dt, x); theta in double, as the
+// reference's `length` is the double literal 1.0.
+// out: rows x (blocks * tpb) samples of 7 floats, row-major (tree[row * tWidth + col]).
+void oracle_random_tree(int kind, const float* root, int rows, int blocks, int tpb, float* out) {
+    const int width = blocks * tpb;
+    const size_t tWidth = (size_t)width * 7;
+    std::vector<oracle::XorwowState> st(kind == 1 ? width : 0);
+    for (int g = 0; g < (int)st.size(); ++g) st[g] = oracle::xorwow_seed((uint64_t)(long long)(g * rows));
+    std::vector<float> x0((size_t)blocks * 4);
+    for (int b = 0; b < blocks; ++b)
+        for (int k = 0; k < 4; ++k) x0[(size_t)b * 4 + k] = root[k];
+    for (int row = 0; row < rows; ++row) {
+        for (int g = 0; g < width; ++g) {
+            const size_t outIndex = (size_t)row * tWidth + (size_t)g * 7;
+            oracle::XorwowState fresh = oracle::xorwow_seed((uint64_t)(long long)(int)outIndex);
+            oracle::XorwowState& rs = kind == 1 ? st[g] : fresh;
+            const float a = fmaf(oracle::xorwow_uniform(rs), 5.0f, -2.5f);
+            const float steering = (float)std::fma((double)oracle::xorwow_uniform(rs), M_PI, -M_PI / 2);
+            const float duration = oracle::xorwow_uniform(rs) * 0.3f;
+            const float dt = duration / 20.0f;
+            const float* p = &x0[(size_t)(g / tpb) * 4];
+            float x = p[0], y = p[1], theta = p[2], v = p[3];
+            const float tn = sbmp::tanf_d(steering);
+            for (int i = 0; i < 20; ++i) {
+                float sn, cs;
+                sbmp::sincosf_d(theta, &sn, &cs);
+                x = fmaf(v * cs, dt, x);
+                y = fmaf(v * sn, dt, y);
+                theta = (float)std::fma((double)v * (double)tn, (double)dt, (double)theta);
+                v = fmaf(a, dt, v);
+            }
+            float* o = &out[outIndex];
+            o[0] = x; o[1] = y; o[2] = theta; o[3] = v; o[4] = a; o[5] = steering; o[6] = duration;
+        }
+        for (int b = 0; b < blocks; ++b)
+            for (int k = 0; k < 4; ++k) x0[(size_t)b * 4 + k] = out[(size_t)row * tWidth + (size_t)b * tpb * 7 + k];
+    }
+}
+
 void oracle_sincosf(const float* x, int n, float* s, float* c) {
     for (int i = 0; i < n; ++i) sbmp::sincosf_d(x[i], &s[i], &c[i]);
 }

@@ -88,6 +88,7 @@ def lib():
         L.oracle_xorwow_draw.argtypes = [vp, i, vp]
         L.oracle_replay.argtypes = [P(OracleParams), vp, i, vp, vp, i, vp, vp]
         L.oracle_sincosf.argtypes = [vp, i, vp, vp]
+        L.oracle_random_tree.argtypes = [i, vp, i, i, i, vp]
         L.oracle_tanf.argtypes = [vp, i, vp]
         _lib = L
     return _lib
@@ -245,6 +246,15 @@ def replay(cfg: PlannerConfig, obstacles, parents: np.ndarray, controls: np.ndar
     lib().oracle_replay(ctypes.byref(p), _fp(obs), len(obs) // 4, _fp(parents), _fp(controls), n, _fp(out),
                         _fp(valid))
     return out, valid.astype(bool)
+
+
+def random_tree(kind: str, root, rows: int, blocks: int, tpb: int) -> np.ndarray:
+    """Legacy generators: kind 'naive' (NaivePlanner.cu) or 'costprop'
+    (CostPropPlanner.cu) -> (rows, blocks * tpb, 7) samples."""
+    r = np.ascontiguousarray(np.asarray(root, dtype=np.float32)[:7])
+    out = np.zeros((rows, blocks * tpb, 7), dtype=np.float32)
+    lib().oracle_random_tree(0 if kind == "naive" else 1, _fp(r), rows, blocks, tpb, _fp(out))
+    return out
 
 
 def xorwow_init(seed: int, subsequence: int, seeding: str = "curand") -> np.ndarray:

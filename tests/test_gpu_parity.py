@@ -293,3 +293,41 @@ def test_obstacle_grid_bit_exact(case, variant, agent, obstacles, oracle_lib, mo
     o.plan(DEMO_INITIAL, DEMO_GOAL, obs, 31)
     assert g.result().iterations > 3
     assert_same_state(g, o, label=f"{case} {agent}")
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_solution_path(seed, d_obs, obstacles, oracle_lib):
+    """Solution extraction: the path root .. goal node equals the
+    oracle tree's parent chain; it starts at the root, ends inside the goal radius
+    and every cost is its parent's cost plus its duration (KGMT.cu:631-633)."""
+    g, cfg, extra = _mk()
+    r = g.plan(DEMO_INITIAL, DEMO_GOAL, d_obs, len(obstacles), seed=seed)
+    o = _oracle(cfg, extra)
+    o.plan(DEMO_INITIAL, DEMO_GOAL, obstacles, seed)
+    s, p, c = o.tree()
+    assert r.goalIndex >= 0, "demo seeds 1-3 solve"
+    want = [r.goalIndex]
+    while p[want[-1]] >= 0:
+        want.append(int(p[want[-1]]))
+    want = want[::-1]
+    rows, samples, costs = g.solution_path()
+    assert rows.tolist() == want and rows[0] == 0
+    assert np.array_equal(bits(samples), bits(s[rows])) and np.array_equal(bits(costs), bits(c[rows]))
+    assert np.hypot(samples[-1, 0] - DEMO_GOAL[0], samples[-1, 1] - DEMO_GOAL[1]) < cfg["goalThreshold"]
+    assert np.array_equal(bits(costs[1:]), bits((costs[:-1] + samples[1:, 6]).astype(np.float32)))
+    assert bits(np.float32(costs[-1])) == bits(np.float32(r.costToGoal))
+    mid = int(rows[len(rows) // 2])   # any row: its own chain
+    r2, _, _ = g.solution_path(mid)
+    assert r2.tolist() == want[:len(want) // 2 + 1]
+    with pytest.raises(RuntimeError):
+        g.solution_path(r.treeSize + 5)
+
+
+def test_solution_path_without_solution(d_obs, obstacles):
+    g, cfg, extra = _mk(numIterations=2)
+    r = g.plan(DEMO_INITIAL, DEMO_GOAL, d_obs, len(obstacles), seed=4)
+    assert r.goalIndex == -1
+    rows, samples, costs = g.solution_path()
+    assert len(rows) == 0 and samples.shape == (0, 7)
+    rows, _, _ = g.solution_path(0)
+    assert rows.tolist() == [0]
