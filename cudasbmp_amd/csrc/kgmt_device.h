@@ -70,6 +70,7 @@ constexpr uint16_t kNoKey = 0xffff;  // child outside the R2 grid (D3)
 // table serialise there and back up the stores of the CUs behind them (k_expand
 // 18.7 -> 14.6 us at 8 replicas).
 constexpr int kDeltaReps = 8;
+constexpr int kRecordF4 = 3;   // sharded record: state, ctrl (a, steer, dur, parent), (block, index in block, -, -)
 
 // Everything a kernel needs, passed by value.
 struct KgmtDev {
@@ -87,19 +88,29 @@ struct KgmtDev {
     // Per-iteration exchange, one fused u64 buffer per direction.
     // *Out is what this rank produced, *In the sum over ranks (RCCL all-reduce, or
     // the local group's sum kernel); on a single rank Out and In are the same memory.
-    // Every field is either disjoint per rank (GNew words and block counts of owned
-    // slots) or a carry-free counter (R1 deltas, R2New bytes), so a sum merges them.
-    unsigned long long* gnewOut;        // accept flags of owned slots (GNew), one bit per slot
-    unsigned long long* gnewIn;         // all ranks' flags (the insert kernels clear it, D6)
-    int* blockCountOut;                 // accepted (+ stale) children per owned 256-slot block
+    // Every exchanged field is either disjoint per rank (rank totals) or a carry-free
+    // counter (R1 deltas, block prefixes, R2New bytes), so a sum merges them.
+    // GNew words and block counts are never exchanged: In and Out are the same
+    // (the owner's) memory, and a sharded rank holds only its owned slots' entries.
+    unsigned long long* gnewOut;        // accept flags (GNew), one bit per slot; cleared by k_finish (D6)
+    unsigned long long* gnewIn;
+    int* blockCountOut;                 // accepted (+ stale) children per 256-slot block
     const int* blockCountIn;
+    // Sharded ranks only (null otherwise), filled by k_pack: pfx[g] = accepted (+ stale)
+    // children of the blocks before g, pfx[nBlocks] = the total (each rank adds the
+    // part of its own blocks, so the sum is global); tot[q] = rank q's record count.
+    int* pfxOut;
+    const int* pfxIn;
+    int* totOut;
+    const int* totIn;
     unsigned long long* deltaOut;       // this iteration's valid (bits 0-31) / invalid (32-63) children per R1 cell
     const unsigned long long* deltaIn;
     uint8_t* r2newOut;                  // 1 = cell seen valid while unavailable in the snapshot
     const uint8_t* r2newIn;
     // Sharded ranks: accepted children packed in owned-slot order by k_pack into a
-    // record buffer [2 parities][recCap][state, ctrl]; the insert kernels of every
-    // rank read them from the owner's buffer (peer memory over xGMI).
+    // record buffer [2 parities][recCap][state, ctrl, (block, index in block)]; the
+    // insert kernels of every rank read them from the owner's buffer (peer memory
+    // over xGMI).  Block counts and GNew words stay with their owner.
     int sharded;
     int recCap;
     float4* recOut;

@@ -181,7 +181,7 @@ __global__ __launch_bounds__(kBlock) void k_expand(KgmtDev d, int t) {
     // the parent-row load follows it directly.
     const uint4 ra = d.rngA[slot];
     const uint2 rb = d.rngB[slot];
-    const unsigned long long oldWord = (lane == 0) ? d.gnewIn[slot >> 6] : 0ull;
+    const unsigned long long oldWord = (lane == 0) ? d.gnewOut[slot >> 6] : 0ull;   // this rank's own words
     const float scoreReg = (tid < d.nR1) ? d.R1Score[(t & 1) * d.nR1 + tid] : 0.0f;
     const float4 obsReg = (kLdsObs && tid < d.nObs) ? d.obstacles[tid] : make_float4(0.f, 0.f, 0.f, 0.f);
     uint32_t snapReg[kMaxR2Words / kBlock];
@@ -381,9 +381,12 @@ __device__ void plan_iteration(const KgmtDev& d, int t, long long* st) {
     // ---- loads
     const IterCtrl pc = d.ctrl[t > 1 ? t - 1 : 0];
     int cnt = 0;
-    for (int i = tid * 4; i < d.nBlocks; i += kBlock * 4) {   // counts are int4-readable
-        const int4 v = *reinterpret_cast<const int4*>(d.blockCountIn + i);
-        cnt += v.x + v.y + v.z + v.w;
+    const int pfxTotal = d.pfxIn ? d.pfxIn[d.nBlocks] : 0;   // sharded: the exchange carries the total
+    if (!d.pfxIn) {
+        for (int i = tid * 4; i < d.nBlocks; i += kBlock * 4) {   // counts are int4-readable
+            const int4 v = *reinterpret_cast<const int4*>(d.blockCountIn + i);
+            cnt += v.x + v.y + v.z + v.w;
+        }
     }
     unsigned long long dv[kDeltaReps];
 #pragma unroll
@@ -409,12 +412,12 @@ __device__ void plan_iteration(const KgmtDev& d, int t, long long* st) {
     }
     sCovInc[tid] = 0;
     int A = 0;
-    if (ranPrev) {   // accepted children of iteration t-1
+    if (ranPrev && !d.pfxIn) {   // accepted children of iteration t-1
         const int wsum = wave_sum(cnt);
         if ((tid & (kWave - 1)) == 0) sRed[0][tid >> 6] = wsum;
     }
     __syncthreads();
-    if (ranPrev) A = sRed[0][0] + sRed[0][1] + sRed[0][2] + sRed[0][3];
+    if (ranPrev) A = d.pfxIn ? pfxTotal : sRed[0][0] + sRed[0][1] + sRed[0][2] + sRed[0][3];
     SBMP_FIN_STAMP(1);
 
     // ---- fold the previous expansion's region deltas (t == 1: all zero)
@@ -572,9 +575,8 @@ __device__ void insert_block(const KgmtDev& d, int t, int gblock, long long* st)
     if (gblock * kBlock >= c.H) return;
     if (myCount == 0) return;   // no accepted (or stale) slot: nothing to insert or clear
     SBMP_FIN_STAMP(1);
-    const int owner = gblock % d.nranks;   // block-cyclic slot ownership
-    int pre, A, preOwner;
-    block_prefix_total(d.blockCountIn, d.nBlocks, gblock, &pre, &A, sRed, d.nranks, owner, &preOwner);
+    int pre, A;
+    block_prefix_total(d.blockCountIn, d.nBlocks, gblock, &pre, &A, sRed);
     SBMP_FIN_STAMP(2);
 
     if (lane == 0) sWaveCnt[wave] = __popcll(word);
@@ -591,15 +593,8 @@ __device__ void insert_block(const KgmtDev& d, int t, int gblock, long long* st)
         const int dst = c.treeSize + j;
         if (j < nIns && dst < d.M) {   // D13: the reference writes past M here
             const int slot = w * kWave + lane;
-            float4 s, u;
-            if (!d.sharded) {
-                s = d.uState[slot];
-                u = d.uCtrl[slot];
-            } else {   // the owner packed its accepted slots in slot order (k_pack)
-                const float4* rec = d.recPeer[owner] + ((size_t)(t & 1) * d.recCap + preOwner + (j - pre)) * 2;
-                s = load_record(rec);
-                u = load_record(rec + 1);
-            }
+            const float4 s = d.uState[slot];
+            const float4 u = d.uCtrl[slot];
             const int parent = __float_as_int(u.w);
             const float cost = d.treeCtrl[parent].w + u.z;   // getCost = duration (KGMT.cu:631-633)
             d.treeState[dst] = s;
@@ -617,16 +612,86 @@ __device__ void insert_block(const KgmtDev& d, int t, int gblock, long long* st)
         unsigned long long nw_ = word;
         if (base + kWave <= cleared) nw_ = 0ull;
         else if (base < cleared) nw_ = word & ~((1ull << (cleared - base)) - 1ull);
-        if (nw_ != word) {
-            d.gnewIn[w] = nw_;
-            if (d.gnewOut != d.gnewIn && owner == d.rank) d.gnewOut[w] = nw_;   // the owner's own view
+        if (nw_ != word) d.gnewIn[w] = nw_;
+    }
+}
+
+// Sharded ranks: iteration t's accepted (and stale, D6) children of
+// every rank, record-driven.  The owners' record lists, concatenated in rank order,
+// are walked with a grid-stride loop; record (block g, index i) becomes row
+// treeSize + pfx[g] + i, its rank in global slot order.  The work is proportional
+// to the accepted count, not to the number of slots or ranks.
+__device__ void insert_records(const KgmtDev& d, int t, int wg, int nWG, long long* st) {
+    const IterCtrl c = d.ctrl[t];
+    if (!c.executed) return;
+    int start[kMaxRanks + 1];
+    start[0] = 0;
+    for (int q = 0; q < d.nranks; ++q) start[q + 1] = start[q] + d.totIn[q];
+    const int A = start[d.nranks];
+    SBMP_FIN_STAMP(1);
+    const int m32 = d.M / 32;
+    const int grid = min(A, m32);   // updateG launch: min(|GNew|, M/32) blocks of 32 (KGMT.cu:231)
+    const int nIns = 32 * grid < A ? 32 * grid : A;
+    for (int i = wg * kBlock + (int)threadIdx.x; i < A; i += nWG * kBlock) {
+        int q = 0;
+        while (q + 1 < d.nranks && i >= start[q + 1]) ++q;
+        const float4* rec = d.recPeer[q] + ((size_t)(t & 1) * d.recCap + (i - start[q])) * kRecordF4;
+        const float4 s = load_record(rec);
+        const float4 u = load_record(rec + 1);
+        const float4 m = load_record(rec + 2);
+        const int j = d.pfxIn[__float_as_int(m.x)] + __float_as_int(m.y);
+        const int dst = c.treeSize + j;
+        if (j < nIns && dst < d.M) {   // D13
+            const int parent = __float_as_int(u.w);
+            const float cost = d.treeCtrl[parent].w + u.z;   // getCost = duration (KGMT.cu:631-633)
+            d.treeState[dst] = s;
+            d.treeCtrl[dst] = make_float4(u.x, u.y, u.z, cost);
+            d.treeParent[dst] = parent;
+            const float dx = s.x - d.goalX, dy = s.y - d.goalY;   // inGoalRegion, KGMT.cu:635-638
+            const float d2 = dx * dx + dy * dy;
+            if (__builtin_sqrtf(d2) < d.goalThreshold) atomicMin(&d.status->goalIdx, dst);
         }
     }
+    SBMP_FIN_STAMP(3);
+}
+
+// Sharded ranks: the D6 clear of GNew[0 .. 32*grid) on this rank's own words (owned
+// block lb; no other rank keeps them).
+__device__ void owner_clear(const KgmtDev& d, int t, int lb) {
+    const int gblock = d.rank + d.nranks * lb;
+    const IterCtrl c = d.ctrl[t];
+    if (!c.executed || gblock * kBlock >= c.H) return;
+    const int w = gblock * (kBlock / kWave) + (int)(threadIdx.x >> 6);
+    if ((threadIdx.x & (kWave - 1)) != 0) return;
+    const unsigned long long word = d.gnewOut[w];
+    if (word == 0ull) return;
+    const int A = d.pfxIn[d.nBlocks];
+    const int grid = min(A, d.M / 32);
+    const long long cleared = d.fixGNewClear ? (1ll << 62) : 32ll * grid;
+    const long long base = (long long)w * kWave;
+    unsigned long long nw_ = word;
+    if (base + kWave <= cleared) nw_ = 0ull;
+    else if (base < cleared) nw_ = word & ~((1ull << (cleared - base)) - 1ull);
+    if (nw_ != word) d.gnewOut[w] = nw_;
 }
 
 // Sharded ranks: this rank's accepted (and stale, D6) children of iteration t in
 // owned-slot order into record buffer t & 1, for the insert kernels of every rank.
 // A block's position is the count over this rank's earlier blocks (local counts).
+// The records are written through to memory (system-scope stores): peers read them
+// over xGMI after the all-reduce that follows this kernel in stream order.  The
+// block also fills its part of the exchange's prefix fields (KgmtDev::pfx / opfx):
+// its owner-local offset, and this rank's share of the global prefix of every block
+// up to its next owned block (the last active block: up to the total), so the
+// all-reduce's sum hands every insert block its offset and the total in O(1).
+__device__ __forceinline__ void store_record(float4* p, float4 v) {
+    unsigned long long* q = reinterpret_cast<unsigned long long*>(p);
+    __hip_atomic_store(q, ((unsigned long long)__float_as_uint(v.y) << 32) | __float_as_uint(v.x), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(q + 1, ((unsigned long long)__float_as_uint(v.w) << 32) | __float_as_uint(v.z),
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 __global__ __launch_bounds__(kBlock) void k_pack(KgmtDev d, int t) {
     __shared__ int sRed[3][kBlock / kWave];
     __shared__ int sWaveCnt[kBlock / kWave];
@@ -646,15 +711,23 @@ __global__ __launch_bounds__(kBlock) void k_pack(KgmtDev d, int t) {
         sWaveCnt[wave] = __popcll(word);
     }
     __syncthreads();
-    int off = sRed[0][0] + sRed[0][1] + sRed[0][2] + sRed[0][3];
-    for (int i = 0; i < wave; ++i) off += sWaveCnt[i];
+    const int preLocal = sRed[0][0] + sRed[0][1] + sRed[0][2] + sRed[0][3];
+    int inBlock = 0;
+    for (int i = 0; i < wave; ++i) inBlock += sWaveCnt[i];
     if ((word >> lane) & 1ull) {
         const int slot = w * kWave + lane;
-        float4* rec = d.recOut + ((size_t)(t & 1) * d.recCap + off + __popcll(word & ((1ull << lane) - 1ull))) * 2;
-        rec[0] = d.uState[slot];
-        rec[1] = d.uCtrl[slot];
+        const int idx = inBlock + __popcll(word & ((1ull << lane) - 1ull));   // index within the block
+        float4* rec = d.recOut + ((size_t)(t & 1) * d.recCap + preLocal + idx) * kRecordF4;
+        store_record(rec, d.uState[slot]);
+        store_record(rec + 1, d.uCtrl[slot]);
+        store_record(rec + 2, make_float4(__int_as_float(gblock), __int_as_float(idx), 0.0f, 0.0f));
     }
-    __threadfence_system();   // peers read these over xGMI after the next all-reduce
+    const int cnt = sWaveCnt[0] + sWaveCnt[1] + sWaveCnt[2] + sWaveCnt[3];
+    const int next = gblock + d.nranks;   // H never decreases: blocks >= H never ran, entries past them are unused
+    const bool last = (long long)next * kBlock >= c.H;
+    const int hi = last ? d.nBlocks : min(next, d.nBlocks);
+    for (int g = gblock + 1 + (int)threadIdx.x; g <= hi; g += kBlock) d.pfxOut[g] = preLocal + cnt;
+    if (last && threadIdx.x == 0) d.totOut[d.rank] = preLocal + cnt;
 }
 
 // Local shard group (P ranks on one device, one stream): the all-reduce of the
@@ -677,8 +750,14 @@ __global__ __launch_bounds__(kBlock) void k_finish(KgmtDev d, int t) {
     const bool tl = d.timelineFin && t == d.timelineIter && threadIdx.x < kWave;
     long long st[kTimelineStamps] = {0, 0, 0, 0, 0, 0, 0, 0};
     if (tl) st[0] = (long long)__builtin_amdgcn_s_memrealtime();
-    if (blockIdx.x == 0) plan_iteration(d, t + 1, tl ? st : nullptr);
-    else insert_block(d, t, (int)blockIdx.x - 1, tl ? st : nullptr);   // every rank inserts every block
+    if (blockIdx.x == 0) {
+        plan_iteration(d, t + 1, tl ? st : nullptr);
+    } else if (d.sharded) {   // every rank inserts every rank's children (replicated tree)
+        insert_records(d, t, (int)blockIdx.x - 1, (int)gridDim.x - 1, tl ? st : nullptr);
+        owner_clear(d, t, (int)blockIdx.x - 1);
+    } else {
+        insert_block(d, t, (int)blockIdx.x - 1, tl ? st : nullptr);
+    }
     if (tl) {
         st[7] = (long long)__builtin_amdgcn_s_memrealtime();
         if (threadIdx.x == 0)

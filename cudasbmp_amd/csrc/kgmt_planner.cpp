@@ -123,25 +123,47 @@ KgmtPlanner::KgmtPlanner(const sbmp_kgmt_params& p, int nranks, int rank, Exchan
     d.R2Valid = alloc<int>(d.nR2);
     d.R2Invalid = alloc<int>(d.nR2);
     d.R1Score = alloc<float>(2 * d.nR1);
-    {   // exchange buffer: [R1 delta replicas | block counts (int4-readable) | GNew words | R2New bytes]
-        const size_t dWords = round_up((long long)kDeltaReps * d.nR1, 2);   // block counts stay 16-B aligned
+    {   // Exchange buffer, one u64 array per direction (16-B aligned fields).
+        // Single rank: [R1 delta replicas | block counts (int4-readable) | GNew words |
+        //               R2New bytes], Out == In.
+        // Sharded: [R1 delta replicas | block prefixes pfx | rank totals | R2New bytes]
+        //          is all-reduced; block counts and GNew words are the owner's alone
+        //          (a separate local buffer), since the inserts are record-driven.
+        const bool sharded = nranks > 1 || ex;
+        const size_t dWords = round_up((long long)kDeltaReps * d.nR1, 2);
         const size_t bcWords = round_up(d.nBlocks, 4) / 2, r2Words = round_up(d.nR2, 16) / 8;
-        xWords_ = dWords + bcWords + (size_t)nWords + r2Words;
+        const size_t pfxWords = round_up(d.nBlocks + 1, 4) / 2, totWords = kMaxRanks / 2;
+        unsigned long long* local = nullptr;
+        if (sharded) {
+            xWords_ = dWords + pfxWords + totWords + r2Words;
+            local = alloc<unsigned long long>(bcWords + (size_t)nWords);
+            localWords_ = bcWords + (size_t)nWords;
+            local_ = local;
+        } else {
+            xWords_ = dWords + bcWords + (size_t)nWords + r2Words;
+        }
         xSend_ = alloc<unsigned long long>(xWords_);
-        xRecv_ = (nranks > 1 || ex) ? alloc<unsigned long long>(xWords_) : xSend_;
+        xRecv_ = sharded ? alloc<unsigned long long>(xWords_) : xSend_;
+        int* bc = reinterpret_cast<int*>(sharded ? local : xSend_ + dWords);
+        unsigned long long* gn = sharded ? local + bcWords : xSend_ + dWords + bcWords;
+        d.blockCountOut = bc;
+        d.blockCountIn = bc;
+        d.gnewOut = gn;
+        d.gnewIn = gn;
         auto views = [&](unsigned long long* x, bool out) {
-            int* bc = reinterpret_cast<int*>(x + dWords);
-            unsigned long long* gn = x + dWords + bcWords;
-            uint8_t* r2 = reinterpret_cast<uint8_t*>(gn + nWords);
+            int* pfx = sharded ? reinterpret_cast<int*>(x + dWords) : nullptr;
+            int* tot = sharded ? reinterpret_cast<int*>(x + dWords + pfxWords) : nullptr;
+            uint8_t* r2 = reinterpret_cast<uint8_t*>(sharded ? x + dWords + pfxWords + totWords
+                                                             : x + dWords + bcWords + nWords);
             if (out) {
                 d.deltaOut = x;
-                d.blockCountOut = bc;
-                d.gnewOut = gn;
+                d.pfxOut = pfx;
+                d.totOut = tot;
                 d.r2newOut = r2;
             } else {
                 d.deltaIn = x;
-                d.blockCountIn = bc;
-                d.gnewIn = gn;
+                d.pfxIn = pfx;
+                d.totIn = tot;
                 d.r2newIn = r2;
             }
         };
@@ -150,7 +172,7 @@ KgmtPlanner::KgmtPlanner(const sbmp_kgmt_params& p, int nranks, int rank, Exchan
     }
     d.sharded = nranks > 1 || ex != nullptr;   // one RCCL rank still takes the sharded path
     d.recCap = expandBlocks_ * kBlock;   // a rank never holds more flagged slots than it owns
-    d.recOut = d.sharded ? alloc<float4>((size_t)4 * d.recCap) : nullptr;
+    d.recOut = d.sharded ? alloc<float4>((size_t)2 * kRecordF4 * d.recCap) : nullptr;
     for (int q = 0; q < kMaxRanks; ++q) d.recPeer[q] = nullptr;
     d.recPeer[rank] = d.recOut;
     d.logSlots = expandBlocks_ * kBlock;
@@ -175,7 +197,7 @@ KgmtPlanner::KgmtPlanner(const sbmp_kgmt_params& p, int nranks, int rank, Exchan
     SBMP_HIP(hipStreamSynchronize(stream_));
     if (d.sharded && ex_) {   // map every rank's record buffer (IPC over xGMI)
         void* peers[kMaxRanks] = {nullptr};
-        ex_->share_buffer(d.recOut, sizeof(float4) * 4 * (size_t)d.recCap, peers);
+        ex_->share_buffer(d.recOut, sizeof(float4) * 2 * kRecordF4 * (size_t)d.recCap, peers);
         for (int q = 0; q < nranks; ++q) d.recPeer[q] = static_cast<const float4*>(peers[q]);
     }
 }
@@ -213,6 +235,7 @@ void KgmtPlanner::begin(const float* initial, const float* goal, const float* d_
     SBMP_HIP(hipMemsetAsync(d.treeCtrl, 0, sizeof(float4) * d.M, s));
     launch_fill_i32(d.treeParent, -1, d.M, s);
     SBMP_HIP(hipMemsetAsync(xSend_, 0, sizeof(unsigned long long) * xWords_, s));
+    if (local_) SBMP_HIP(hipMemsetAsync(local_, 0, sizeof(unsigned long long) * localWords_, s));
     if (xRecv_ != xSend_) SBMP_HIP(hipMemsetAsync(xRecv_, 0, sizeof(unsigned long long) * xWords_, s));
     for (int* a : {d.R1, d.R1Avail, d.R1Valid, d.R1Invalid, d.R1Cov})
         SBMP_HIP(hipMemsetAsync(a, 0, sizeof(int) * d.nR1, s));
@@ -322,7 +345,11 @@ void KgmtPlanner::stage_exchange() {
     if (ex_) ex_->allreduce_u64(xSend_, xRecv_, xWords_, stream_);
 }
 
-void KgmtPlanner::stage_finish(int t) { launch_finish(d_, t, d_.nBlocks, stream_, timing(K_FINISH)); }
+void KgmtPlanner::stage_finish(int t) {
+    // single rank: one insert block per 256-slot block; sharded: the record-driven
+    // insert and the owner's GNew clear, one block per owned block
+    launch_finish(d_, t, d_.sharded ? expandBlocks_ : d_.nBlocks, stream_, timing(K_FINISH));
+}
 
 void KgmtPlanner::stage_fold(int t) {
     if (t - lastFolded_ >= kFoldEvery) fold_to(t);
@@ -542,7 +569,16 @@ void KgmtPlanner::copy_flags(uint8_t* G, uint8_t* GNew) {
     }
     if (GNew) {
         std::vector<unsigned long long> w(d_.nWords);
-        SBMP_HIP(hipMemcpy(w.data(), d_.gnewIn, sizeof(unsigned long long) * d_.nWords, hipMemcpyDeviceToHost));
+        if (ex_ && d_.nranks > 1) {   // each rank holds its owned words (zero elsewhere): the sum merges
+            unsigned long long* tmp = nullptr;
+            SBMP_HIP(hipMalloc(&tmp, sizeof(unsigned long long) * d_.nWords));
+            ex_->allreduce_u64(d_.gnewOut, tmp, d_.nWords, stream_);
+            SBMP_HIP(hipStreamSynchronize(stream_));
+            SBMP_HIP(hipMemcpy(w.data(), tmp, sizeof(unsigned long long) * d_.nWords, hipMemcpyDeviceToHost));
+            (void)hipFree(tmp);
+        } else {
+            SBMP_HIP(hipMemcpy(w.data(), d_.gnewOut, sizeof(unsigned long long) * d_.nWords, hipMemcpyDeviceToHost));
+        }
         memset(GNew, 0, M);
         for (int s = 0; s < d_.nSlots; ++s) GNew[s] = (w[s >> 6] >> (s & 63)) & 1ull;
     }

@@ -151,6 +151,8 @@ private:
     int expandVariant_ = 0;   // SBMP_EXPAND_VARIANT: obstacle form, 0 = auto (3 if <= kMaxRegObs boxes, else 1)
     bool timelineDumped_ = false;
     int lastFolded_ = 0;      // iterations <= lastFolded_ are in R2Valid / R2Invalid
+    unsigned long long* local_ = nullptr;   // sharded: the owner's block counts + GNew words
+    size_t localWords_ = 0;
     unsigned long long* xSend_ = nullptr;
     unsigned long long* xRecv_ = nullptr;
     size_t xWords_ = 0;
@@ -197,7 +199,7 @@ public:
 
     void copy_tree(float* samples, int* parent, float* costs) override { r0().copy_tree(samples, parent, costs); }
     void copy_unexplored(float* samples, int* uParent) override;
-    void copy_flags(uint8_t* G, uint8_t* GNew) override { r0().copy_flags(G, GNew); }
+    void copy_flags(uint8_t* G, uint8_t* GNew) override;   // GNew words live with their owner
     void copy_regions(int* R1, int* R1Avail, int* R1Valid, int* R1Invalid, float* R1Score, int* R2Avail,
                       int* R2Valid, int* R2Invalid) override;
     void copy_rng(uint32_t* states) override;

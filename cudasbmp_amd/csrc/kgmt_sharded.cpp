@@ -172,6 +172,16 @@ void LocalShardGroup::copy_rng(uint32_t* states) {
     }
 }
 
+void LocalShardGroup::copy_flags(uint8_t* G, uint8_t* GNew) {
+    r0().copy_flags(G, GNew);
+    if (!GNew) return;
+    std::vector<uint8_t> f(params().maxTreeSize);
+    for (size_t q = 1; q < ranks_.size(); ++q) {   // non-owned words are zero on every rank
+        ranks_[q]->copy_flags(nullptr, f.data());
+        for (size_t i = 0; i < f.size(); ++i) GNew[i] |= f[i];
+    }
+}
+
 // R2Valid / R2Invalid: each rank folded the children of its own slots.
 void LocalShardGroup::copy_regions(int* R1, int* R1Avail, int* R1Valid, int* R1Invalid, float* R1Score, int* R2Avail,
                                    int* R2Valid, int* R2Invalid) {
