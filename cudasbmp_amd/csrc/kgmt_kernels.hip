@@ -56,8 +56,11 @@ typedef int sbmp_i32x16 __attribute__((ext_vector_type(16)));
 __device__ __forceinline__ IterCtrl load_ctrl(const IterCtrl* p, const PlannerStatus* st, int* goalIdx) {
     sbmp_i32x16 v;
     int g;
+    // Early-clobber outputs: the second load must not take its address from registers
+    // the first one is filling (it did: the status address landed inside v, and a
+    // fast return of the control block turned it into a wild pointer).
     asm volatile("s_load_dwordx16 %0, %2, 0x0\n\ts_load_dword %1, %3, 0x0\n\ts_waitcnt lgkmcnt(0)"
-                 : "=s"(v), "=s"(g)
+                 : "=&s"(v), "=&s"(g)
                  : "s"(p), "s"(st)
                  : "memory");
     *goalIdx = g;
