@@ -70,6 +70,7 @@ constexpr uint16_t kNoKey = 0xffff;  // child outside the R2 grid (D3)
 // table serialise there and back up the stores of the CUs behind them (k_expand
 // 18.7 -> 14.6 us at 8 replicas).
 constexpr int kDeltaReps = 8;
+constexpr int kInsertBase = 8;   // k_finish workgroup of insert block 0 (one per XCD ahead of it)
 constexpr int kRecordF4 = 3;   // sharded record: state, ctrl (a, steer, dur, parent), (block, index in block, -, -)
 
 // Everything a kernel needs, passed by value.

@@ -85,41 +85,6 @@ __device__ __forceinline__ int wave_sum(int v) {
     return v;
 }
 
-// Sum of counts[0, nb) and of counts[0, mine) over a 256-thread block, and of the
-// entries before `mine` whose index is owner mod nranks (the owner's earlier
-// blocks).  counts is allocated with a multiple-of-4 length and zero beyond every
-// written entry.
-__device__ __forceinline__ void block_prefix_total(const int* __restrict__ counts, int nb, int mine, int* pre,
-                                                   int* tot, int (*sRed)[kBlock / kWave], int nranks = 1,
-                                                   int owner = 0, int* preOwner = nullptr) {
-    int p = 0, s = 0, po = 0;
-    const int nb4 = (nb + 3) & ~3;
-    for (int i = threadIdx.x * 4; i < nb4; i += kBlock * 4) {
-        const int4 v = *reinterpret_cast<const int4*>(counts + i);
-        const int e[4] = {v.x, v.y, v.z, v.w};
-        s += v.x + v.y + v.z + v.w;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const bool before = i + k < mine;
-            p += before ? e[k] : 0;
-            po += (before && (i + k) % nranks == owner) ? e[k] : 0;
-        }
-    }
-    p = wave_sum(p);
-    s = wave_sum(s);
-    po = wave_sum(po);
-    const int wave = threadIdx.x >> 6;
-    if ((threadIdx.x & (kWave - 1)) == 0) {
-        sRed[0][wave] = p;
-        sRed[1][wave] = s;
-        sRed[2][wave] = po;
-    }
-    __syncthreads();
-    *pre = sRed[0][0] + sRed[0][1] + sRed[0][2] + sRed[0][3];
-    *tot = sRed[1][0] + sRed[1][1] + sRed[1][2] + sRed[1][3];
-    if (preOwner) *preOwner = sRed[2][0] + sRed[2][1] + sRed[2][2] + sRed[2][3];
-}
-
 // A record of a peer rank (or of this device, same code): system-scope loads bypass
 // this GPU's caches, which may hold lines of the same parity buffer from two
 // iterations ago.
@@ -372,7 +337,6 @@ __device__ __forceinline__ void batch_rule(const KgmtDev& d, int treeSize, int n
 __device__ void plan_iteration(const KgmtDev& d, int t, long long* st) {
     __shared__ int sRed[3][kBlock / kWave];
     __shared__ int sCovInc[kMaxR1];
-    __shared__ float sScore[kMaxR1];
     __shared__ float sPart[8];
     constexpr int kW = kMaxR2Words / kBlock;
 
@@ -516,27 +480,20 @@ __device__ void plan_iteration(const KgmtDev& d, int t, long long* st) {
             const double den = (double)(1.0f + covR) * (1.0 + r * r);
             sc = (float)((double)fv4 / den);
         }
-        sScore[tid] = own ? sc : 0.0f;
-        __syncthreads();
-        if (tid < 8) {   // CUB BlockReduce order (D8): balanced tree per 32 group ...
-            float tt[32];
+        // CUB BlockReduce order (D8): a shuffle-down tree (offsets 1, 2, 4, 8, 16) per
+        // 32-lane group, then the 8 group sums in order.
+        float v = own ? sc : 0.0f;
 #pragma unroll
-            for (int i = 0; i < 32; ++i) tt[i] = sScore[tid * 32 + i];
-#pragma unroll
-            for (int off = 1; off < 32; off <<= 1) {
-#pragma unroll
-                for (int i = 0; i + off < 32; i += 2 * off) tt[i] = tt[i] + tt[i + off];
-            }
-            sPart[tid] = tt[0];
+        for (int off = 1; off < 32; off <<= 1) {
+            const float o = __shfl_down(v, off, 32);
+            v = v + o;
         }
+        if ((tid & 31) == 0) sPart[tid >> 5] = v;
         __syncthreads();
-        if (tid == 0) {   // ... then the warp aggregates in order
-            float total = sPart[0];
-            for (int w = 1; w < 8; ++w) total = total + sPart[w];
-            sPart[0] = total;
-        }
-        __syncthreads();
-        const float total = sPart[0];
+        float tsum = sPart[0];
+#pragma unroll
+        for (int w = 1; w < 8; ++w) tsum = tsum + sPart[w];
+        const float total = tsum;
         SBMP_FIN_STAMP(3);
         if (own) d.R1Score[buf * d.nR1 + cell] = (r1a == 0) ? 1.0f : sc / total;
     }
@@ -564,26 +521,63 @@ __device__ void plan_iteration(const KgmtDev& d, int t, long long* st) {
 // partial GNew clear (D6).  The block's j offset is the sum of the GNew counts of
 // the blocks before it (counts written by k_expand(t)).
 __device__ void insert_block(const KgmtDev& d, int t, int gblock, long long* st) {
-    __shared__ int sRed[3][kBlock / kWave];
+    __shared__ int sRed[2][kBlock / kWave];
     __shared__ int sWaveCnt[kBlock / kWave];
     const int lane = threadIdx.x & (kWave - 1);
     const int wave = threadIdx.x >> 6;
     const int w = gblock * (kBlock / kWave) + wave;
-    // Loads that do not depend on the control block go first (blockCount entries at
-    // or past the high-water block were never written and are zero).
+    const int slot = w * kWave + lane;
+    // Every load that depends on nothing else is issued first: the flag word, the
+    // block counts (the first 1,024 as one int4 per thread; counts at or past the
+    // high-water block were never written and are zero) and the control block.
     const unsigned long long word = d.gnewIn[w];
     const int myCount = d.blockCountIn[gblock];
+    const int nb4 = (d.nBlocks + 3) & ~3;
+    const int i0 = min((int)threadIdx.x * 4, nb4 - 4);
+    const int4 c0 = *reinterpret_cast<const int4*>(d.blockCountIn + i0);
     const IterCtrl c = d.ctrl[t];
     if (!c.executed) return;
     if (gblock * kBlock >= c.H) return;
     if (myCount == 0) return;   // no accepted (or stale) slot: nothing to insert or clear
     SBMP_FIN_STAMP(1);
-    int pre, A;
-    block_prefix_total(d.blockCountIn, d.nBlocks, gblock, &pre, &A, sRed);
-    SBMP_FIN_STAMP(2);
-
-    if (lane == 0) sWaveCnt[wave] = __popcll(word);
+    // The flagged lanes' children (this XCD wrote them, see k_finish), in flight
+    // while the prefix is reduced.
+    const bool flagged = (word >> lane) & 1ull;
+    float4 us = make_float4(0.f, 0.f, 0.f, 0.f), uc = us;
+    if (flagged) {
+        us = d.uState[slot];
+        uc = d.uCtrl[slot];
+    }
+    // exclusive prefix of this block and the total, over the block counts
+    int p = 0, tot = 0;
+    if ((int)threadIdx.x * 4 < nb4) {
+        const int e[4] = {c0.x, c0.y, c0.z, c0.w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            tot += e[k];
+            p += (i0 + k < gblock) ? e[k] : 0;
+        }
+    }
+    for (int i = (int)threadIdx.x * 4 + kBlock * 4; i < nb4; i += kBlock * 4) {   // more than 1,024 blocks
+        const int4 v = *reinterpret_cast<const int4*>(d.blockCountIn + i);
+        const int e[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            tot += e[k];
+            p += (i + k < gblock) ? e[k] : 0;
+        }
+    }
+    p = wave_sum(p);
+    tot = wave_sum(tot);
+    if (lane == 0) {
+        sRed[0][wave] = p;
+        sRed[1][wave] = tot;
+        sWaveCnt[wave] = __popcll(word);
+    }
     __syncthreads();
+    const int pre = sRed[0][0] + sRed[0][1] + sRed[0][2] + sRed[0][3];
+    const int A = sRed[1][0] + sRed[1][1] + sRed[1][2] + sRed[1][3];
+    SBMP_FIN_STAMP(2);
     int waveOff = pre;
     for (int i = 0; i < wave; ++i) waveOff += sWaveCnt[i];
     if (word == 0ull) return;
@@ -591,19 +585,16 @@ __device__ void insert_block(const KgmtDev& d, int t, int gblock, long long* st)
     const int m32 = d.M / 32;
     const int grid = min(A, m32);   // updateG launch: min(|GNew|, M/32) blocks of 32 (KGMT.cu:231)
     const int nIns = 32 * grid < A ? 32 * grid : A;
-    if ((word >> lane) & 1ull) {
+    if (flagged) {
         const int j = waveOff + __popcll(word & ((1ull << lane) - 1ull));
         const int dst = c.treeSize + j;
         if (j < nIns && dst < d.M) {   // D13: the reference writes past M here
-            const int slot = w * kWave + lane;
-            const float4 s = d.uState[slot];
-            const float4 u = d.uCtrl[slot];
-            const int parent = __float_as_int(u.w);
-            const float cost = d.treeCtrl[parent].w + u.z;   // getCost = duration (KGMT.cu:631-633)
-            d.treeState[dst] = s;
-            d.treeCtrl[dst] = make_float4(u.x, u.y, u.z, cost);
+            const int parent = __float_as_int(uc.w);
+            const float cost = d.treeCtrl[parent].w + uc.z;   // getCost = duration (KGMT.cu:631-633)
+            d.treeState[dst] = us;
+            d.treeCtrl[dst] = make_float4(uc.x, uc.y, uc.z, cost);
             d.treeParent[dst] = parent;
-            const float dx = s.x - d.goalX, dy = s.y - d.goalY;   // inGoalRegion, KGMT.cu:635-638
+            const float dx = us.x - d.goalX, dy = us.y - d.goalY;   // inGoalRegion, KGMT.cu:635-638
             const float d2 = dx * dx + dy * dy;
             if (__builtin_sqrtf(d2) < d.goalThreshold) atomicMin(&d.status->goalIdx, dst);
         }
@@ -747,7 +738,10 @@ __global__ void k_xsum(XsumArgs a, int nranks, long long n) {
     }
 }
 
-// k_finish(t): block 0 prepares iteration t+1, blocks 1.. insert iteration t.
+// k_finish(t): block 0 prepares iteration t+1, the others insert iteration t.  On a
+// single rank, 256-slot block g is inserted by workgroup kInsertBase + g: workgroups
+// are dealt to the 8 XCDs round-robin, so that is the XCD whose k_expand workgroup g
+// just wrote the slots (its L2 holds them).
 __global__ __launch_bounds__(kBlock) void k_finish(KgmtDev d, int t) {
     // Diagnostics (tools/timeline.py --finish): stamps of wave 0, kept in registers.
     const bool tl = d.timelineFin && t == d.timelineIter && threadIdx.x < kWave;
@@ -758,8 +752,8 @@ __global__ __launch_bounds__(kBlock) void k_finish(KgmtDev d, int t) {
     } else if (d.sharded) {   // every rank inserts every rank's children (replicated tree)
         insert_records(d, t, (int)blockIdx.x - 1, (int)gridDim.x - 1, tl ? st : nullptr);
         owner_clear(d, t, (int)blockIdx.x - 1);
-    } else {
-        insert_block(d, t, (int)blockIdx.x - 1, tl ? st : nullptr);
+    } else if (blockIdx.x >= kInsertBase) {   // blocks 1 .. kInsertBase-1 are idle
+        insert_block(d, t, (int)blockIdx.x - kInsertBase, tl ? st : nullptr);
     }
     if (tl) {
         st[7] = (long long)__builtin_amdgcn_s_memrealtime();

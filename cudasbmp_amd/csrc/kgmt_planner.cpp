@@ -348,7 +348,7 @@ void KgmtPlanner::stage_exchange() {
 void KgmtPlanner::stage_finish(int t) {
     // single rank: one insert block per 256-slot block; sharded: the record-driven
     // insert and the owner's GNew clear, one block per owned block
-    launch_finish(d_, t, d_.sharded ? expandBlocks_ : d_.nBlocks, stream_, timing(K_FINISH));
+    launch_finish(d_, t, d_.sharded ? expandBlocks_ : kInsertBase - 1 + d_.nBlocks, stream_, timing(K_FINISH));
 }
 
 void KgmtPlanner::stage_fold(int t) {
