@@ -47,7 +47,8 @@ static_assert(sizeof(IterCtrl) == 64, "IterCtrl is one 64-B line");
 
 struct PlannerStatus {
     int goalIdx;    // lowest tree row inside the goal radius (kNoGoal if none), D4
-    int pad[15];
+    int error;      // nonzero: a k_step hand-off timed out (the host raises it)
+    int pad[14];
 };
 
 constexpr int kMaxLdsObs = 2048;     // obstacle lists up to 32 KB are staged in LDS per block
@@ -70,6 +71,10 @@ constexpr uint16_t kNoKey = 0xffff;  // child outside the R2 grid (D3)
 // table serialise there and back up the stores of the CUs behind them (k_expand
 // 18.7 -> 14.6 us at 8 replicas).
 constexpr int kDeltaReps = 8;
+constexpr int kMaxStepBlocks = 1024;   // k_step: one int4 of block counts per thread (<= 262,144 slots)
+constexpr int kNoGoalIdx = 0x7fffffff;
+constexpr int kStepEntry = 3;       // k_step list entry: state, (a, steer, dur, parent), (cost, -, -, -)
+constexpr int kStepPrefetch = 2;    // snapshot words per thread prefetched before propagation (nR2 <= 16,384)
 constexpr int kInsertBase = 8;   // k_finish workgroup of insert block 0 (one per XCD ahead of it)
 constexpr int kRecordF4 = 3;   // sharded record: state, ctrl (a, steer, dur, parent), (block, index in block, -, -)
 
@@ -116,12 +121,24 @@ struct KgmtDev {
     int recCap;
     float4* recOut;
     const float4* recPeer[kMaxRanks];
+    // Region tables: R1, R1Avail, R1Valid, R1Invalid, R1Cov are the parity-0 slices
+    // of one int array [2][5][nR1], R2Avail of [2][nR2/32].  k_finish updates parity
+    // 0 in place; k_step (below) reads iteration t-1's parity and writes t's.
     int* R1;
     int* R1Avail;
     int* R1Valid;
     int* R1Invalid;
     int* R1Cov;           // available R2 cells per R1 cell (covR numerator, kept incrementally)
     uint32_t* R2Avail;    // live availability bits
+    // k_step (single rank, one launch per iteration): parity [t & 1]
+    // or ring [t % 3] buffers of what iteration t hands to t + 1.
+    int stepMode;
+    int* stepCnt;         // [2][kMaxStepBlocks] per 256-slot block: flagged children | (1 + lowest
+                          // in-block index of a flagged child in the goal region, 0 if none) << 16
+    float4* stepList;     // [2][nBlocks * kBlock][kStepEntry] flagged children compacted per block
+    unsigned long long* stepDelta;   // [3][kDeltaReps * nR1] packed R1 deltas
+    uint32_t* stepR2New;  // [3][nR2 / 32] R2New bits
+    unsigned long long* stepPub;     // [2][nR1 + nR2 / 32] scores and snapshot words, each tagged with t
     uint32_t* R2Snap;     // availability bits at the iteration start (D2)
     int* R2Valid;
     int* R2Invalid;

@@ -762,6 +762,542 @@ __global__ __launch_bounds__(kBlock) void k_finish(KgmtDev d, int t) {
     }
 }
 
+// ------------------------------------------------------------------ step
+// k_step(t): one launch per iteration on a single rank, doing what
+// k_finish(t-1) and k_expand(t) do without the launch between them.
+//   Workgroup 0 (dispatched first, never waits) is the planner: it folds t-1's
+//   region deltas into the tables of parity t & 1, computes the R2 snapshot and
+//   the scores (updateR1), persists ctrl[t], and publishes scores and snapshot as
+//   8-B words tagged with t.
+//   Workgroups 1..nBlocks (block b = blockIdx - 1) each scan t-1's packed block
+//   counts into LDS and derive the same plan scalars; expand their 256 slots -- a
+//   parent row inserted by t-1 is read from t-1's compacted list of the block that
+//   produced it (binary search of the LDS prefix), any older row from the tree --
+//   then take the published scores and snapshot (re-reading until every tag is t,
+//   bounded), run the accept test and write their outputs for t+1: the packed count
+//   and goal index and the compacted list (parity t & 1), R1 deltas and R2New bits
+//   (ring t % 3).  Each also inserts its own block's flagged children of t-1 (rows
+//   treeSize(t-1) + prefix + index) and applies the D6 clear to its words.
+// expand == 0 is the flush pass run before a read-back (no expansion; the same
+// values are rewritten by k_step(t) proper, so it is idempotent).
+__device__ __forceinline__ void step_unpack(int v, int* cnt, int* goal) {
+    *cnt = v & 0xffff;
+    *goal = (v >> 16) - 1;
+}
+
+// Scan of iteration t-1's packed block counts (4 per thread, kMaxStepBlocks = 4 x
+// kBlock): sPfx[g] = flagged children of the blocks before g (g <= nBlocks), *A the
+// total, *jGoal the lowest global index of a flagged child in the goal region.
+__device__ __forceinline__ void step_scan(const KgmtDev& d, int4 pk, int* sPfx, int (*sRed)[kBlock / kWave], int* A,
+                                          int* jGoal) {
+    const int tid = threadIdx.x;
+    const int lane = tid & (kWave - 1);
+    const int wave = tid >> 6;
+    int loc[4], gl4[4];
+    int run = 0;
+    const int v4[4] = {pk.x, pk.y, pk.z, pk.w};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+        int c, g;
+        step_unpack(v4[e], &c, &g);
+        loc[e] = run;
+        gl4[e] = g;
+        run += c;
+    }
+    int incl = run;
+#pragma unroll
+    for (int off = 1; off < kWave; off <<= 1) {
+        const int o = __shfl_up(incl, off, kWave);
+        if (lane >= off) incl += o;
+    }
+    if (lane == kWave - 1) sRed[0][wave] = incl;
+    __syncthreads();
+    int base = incl - run;
+    for (int w = 0; w < wave; ++w) base += sRed[0][w];
+    *A = sRed[0][0] + sRed[0][1] + sRed[0][2] + sRed[0][3];
+    int gmin = kNoGoalIdx;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+        const int g = tid * 4 + e;
+        const int pf = base + loc[e];
+        if (g <= d.nBlocks) sPfx[g] = pf;
+        if (gl4[e] >= 0) gmin = min(gmin, pf + gl4[e]);
+    }
+    if (tid == kBlock - 1 && d.nBlocks == kMaxStepBlocks) sPfx[kMaxStepBlocks] = *A;
+#pragma unroll
+    for (int off = kWave / 2; off > 0; off >>= 1) gmin = min(gmin, __shfl_xor(gmin, off, kWave));
+    if (lane == 0) sRed[1][wave] = gmin;
+    __syncthreads();
+    *jGoal = min(min(sRed[1][0], sRed[1][1]), min(sRed[1][2], sRed[1][3]));
+}
+
+// Plan scalars of iteration t from t-1's control block and the scan (KGMT.cu:118,
+// 139-188,249-259); every workgroup derives the same values.
+struct StepPlan {
+    bool ranPrev;
+    int tsPrev, treeSize, gLo, H, grid, nIns, newGoal, runT, nG, k, nExp, S;
+    bool executes;
+};
+__device__ __forceinline__ StepPlan step_plan(const KgmtDev& d, int t, int expand, const IterCtrl& pc, int goalIdx,
+                                              int A, int jGoal) {
+    StepPlan q;
+    q.ranPrev = (t == 1) || pc.executed;
+    q.tsPrev = (t == 1) ? 1 : pc.treeSize;
+    q.treeSize = (t == 1) ? 1 : pc.treeSize + A;   // KGMT.cu:249
+    q.gLo = (t == 1) ? 0 : pc.gLo + pc.nExp;
+    const int Hprev = (t == 1) ? 0 : pc.H;
+    q.grid = min(A, d.M / 32);   // updateG launch: min(|GNew|, M/32) blocks of 32 (KGMT.cu:231)
+    q.nIns = 32 * q.grid < A ? 32 * q.grid : A;
+    // The lowest inserted row of t-1 inside the goal radius (D4): rows grow with j,
+    // so if the lowest candidate is not inserted (D13) none is.
+    q.newGoal = goalIdx;
+    if (jGoal < q.nIns && (long long)q.tsPrev + jGoal < d.M) q.newGoal = min(q.newGoal, q.tsPrev + jGoal);
+    q.runT = (t <= d.numIterations) && (q.treeSize < d.M);   // KGMT.cu:118,255
+    q.nG = 0;
+    q.k = 0;
+    q.nExp = 0;
+    if (q.runT) {
+        q.nG = q.treeSize - q.gLo;
+        batch_rule(d, q.treeSize, q.nG, &q.k, &q.nExp);
+    }
+    q.S = q.k * q.nExp;
+    q.H = max(Hprev, q.S);
+    q.executes = expand && q.runT && q.newGoal == kNoGoal;
+    return q;
+}
+
+// Workgroup 0 of k_step(t): tables of t (R1 deltas folded, R2New merged into R2Avail
+// = the snapshot, R1Cov), scores (updateR1, KGMT.cu:485-538, CUB order D8), ctrl[t];
+// scores and snapshot published as 8-B words tagged with t.
+__device__ __forceinline__ void step_planner(const KgmtDev& d, int t, int expand, int* sPfx,
+                                             int (*sRed)[kBlock / kWave], int* sCovInc, float* sPart) {
+    constexpr int kW = kMaxR2Words / kBlock;
+    const int tid = threadIdx.x;
+    const int nW = d.nR2 >> 5;
+    const int nn = d.n * d.n;
+    const int pp = (t - 1) & 1, cp = t & 1;
+    const int cell = min(tid, d.nR1 - 1);
+    const bool own = tid < d.nR1;
+    const bool tl = d.timelineFin && t == d.timelineIter && tid == 0;   // diagnostics: entry, publish
+    if (tl) d.timelineFin[0] = (long long)__builtin_amdgcn_s_memrealtime();
+    // every input at entry
+    const int4 pk = *reinterpret_cast<const int4*>(d.stepCnt + (size_t)pp * kMaxStepBlocks + tid * 4);
+    const IterCtrl pc = d.ctrl[t - 1];
+    const int goalIdx = d.status->goalIdx;
+    const int* tabPrev = d.R1 + (size_t)pp * 5 * d.nR1;
+    int r1 = tabPrev[cell], r1a = tabPrev[d.nR1 + cell], r1v = tabPrev[2 * d.nR1 + cell],
+        r1i = tabPrev[3 * d.nR1 + cell], r1c = tabPrev[4 * d.nR1 + cell];
+    const unsigned long long* deltaPrev = d.stepDelta + (size_t)((t - 1) % 3) * kDeltaReps * d.nR1;
+    unsigned long long dl = 0ull;   // replicas: carry-free sums
+#pragma unroll
+    for (int r = 0; r < kDeltaReps; ++r) dl += deltaPrev[(size_t)r * d.nR1 + cell];
+    const uint32_t* availPrev = d.R2Avail + (size_t)pp * nW;
+    const uint32_t* newPrev = d.stepR2New + (size_t)((t - 1) % 3) * nW;
+    uint32_t availW[kW], newW[kW];
+#pragma unroll
+    for (int j = 0; j < kW; ++j) {
+        const int w = min(tid + j * kBlock, nW - 1);
+        availW[j] = availPrev[w];
+        newW[j] = newPrev[w];
+    }
+    for (int i = tid; i < d.nR1; i += kBlock) sCovInc[i] = 0;
+    int A, jGoal;
+    step_scan(d, pk, sPfx, sRed, &A, &jGoal);
+    const StepPlan q = step_plan(d, t, expand, pc, goalIdx, A, jGoal);
+    int* tabCur = d.R1 + (size_t)cp * 5 * d.nR1;
+    if (!q.ranPrev) {   // t-1 did not run: the loop has ended; carry the tables forward
+        for (int i = tid; i < 5 * d.nR1; i += kBlock) tabCur[i] = tabPrev[i];
+        for (int i = tid; i < nW; i += kBlock) d.R2Avail[(size_t)cp * nW + i] = availPrev[i];
+        if (tid == 0) {
+            IterCtrl c{};
+            c.run = 0;
+            c.H = pc.H;
+            d.ctrl[t] = c;
+        }
+        return;
+    }
+    const int nv = (int)(dl & 0xffffffffull), ni = (int)(dl >> 32);
+    r1 += nv + ni;      // KGMT.cu:392
+    r1v += nv;          // KGMT.cu:406
+    r1i += ni;          // KGMT.cu:409
+    if (nv) r1a = 1;    // KGMT.cu:399-401
+    uint32_t snapW[kW];
+#pragma unroll
+    for (int j = 0; j < kW; ++j) {
+        const int w = tid + j * kBlock;
+        snapW[j] = 0u;
+        if (j * kBlock < nW && w < nW) {
+            const uint32_t fresh = newW[j] & ~availW[j];
+            snapW[j] = availW[j] | newW[j];   // R2Avail of t = the snapshot (D2)
+            if (fresh && nn % 32 == 0) {
+                atomicAdd(&sCovInc[(32 * w) / nn], __popc(fresh));
+            } else {
+                uint32_t f = fresh;
+                while (f) {
+                    const int b = __builtin_ctz(f);
+                    f &= f - 1u;
+                    atomicAdd(&sCovInc[(32 * w + b) / nn], 1);
+                }
+            }
+        }
+    }
+    __syncthreads();
+    r1c += sCovInc[cell];
+    float scv = 1.0f;
+    if (q.runT) {
+        float sc = 0.0f;
+        if (r1a != 0) {
+            const float covR = (float)r1c / (float)nn;
+            const float freeVol = (0.01f + (float)r1v) / (0.01f + (float)r1v + (float)r1i);
+            const float fv2 = freeVol * freeVol;
+            const float fv4 = fv2 * fv2;
+            const double rr = (double)r1;
+            const double den = (double)(1.0f + covR) * (1.0 + rr * rr);
+            sc = (float)((double)fv4 / den);
+        }
+        float v = own ? sc : 0.0f;
+#pragma unroll
+        for (int off = 1; off < 32; off <<= 1) {
+            const float o = __shfl_down(v, off, 32);
+            v = v + o;
+        }
+        if ((tid & 31) == 0) sPart[tid >> 5] = v;
+        __syncthreads();
+        float total = sPart[0];
+#pragma unroll
+        for (int w = 1; w < 8; ++w) total = total + sPart[w];
+        scv = (r1a == 0) ? 1.0f : sc / total;
+    }
+    // publish first (tagged 8-B words, written through)
+    unsigned long long* const pub = d.stepPub + (size_t)cp * (d.nR1 + nW);
+    const unsigned long long tag = (unsigned long long)(unsigned)t << 32;
+    if (q.executes) {
+        if (own) __hip_atomic_store(pub + cell, tag | __float_as_uint(scv), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+        for (int j = 0; j < kW; ++j) {
+            const int w = tid + j * kBlock;
+            if (j * kBlock < nW && w < nW)
+                __hip_atomic_store(pub + d.nR1 + w, tag | snapW[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+    if (tl) d.timelineFin[1] = (long long)__builtin_amdgcn_s_memrealtime();
+    if (own) {
+        tabCur[cell] = r1;
+        tabCur[d.nR1 + cell] = r1a;
+        tabCur[2 * d.nR1 + cell] = r1v;
+        tabCur[3 * d.nR1 + cell] = r1i;
+        tabCur[4 * d.nR1 + cell] = r1c;
+        if (q.runT) d.R1Score[cp * d.nR1 + cell] = scv;
+    }
+#pragma unroll
+    for (int j = 0; j < kW; ++j) {
+        const int w = tid + j * kBlock;
+        if (j * kBlock < nW && w < nW) d.R2Avail[(size_t)cp * nW + w] = snapW[j];
+    }
+    {   // ring (t+1) % 3, last read by k_step(t-1): zero for k_step(t+1)
+        unsigned long long* zd = d.stepDelta + (size_t)((t + 1) % 3) * kDeltaReps * d.nR1;
+        for (int i = tid; i < kDeltaReps * d.nR1; i += kBlock) zd[i] = 0ull;
+        uint32_t* zn = d.stepR2New + (size_t)((t + 1) % 3) * nW;
+        for (int i = tid; i < nW; i += kBlock) zn[i] = 0u;
+    }
+    if (tid == 0) {
+        IterCtrl c;
+        c.run = q.runT;
+        c.executed = q.executes ? 1 : 0;
+        c.treeSize = q.treeSize;
+        c.gLo = q.gLo;
+        c.nG = q.nG;
+        c.k = q.k;
+        c.nExp = q.nExp;
+        c.S = q.S;
+        c.H = q.H;
+        c.A = 0;
+        c.scoreBuf = cp;
+        for (int i = 0; i < 5; ++i) c.pad[i] = 0;
+        d.ctrl[t] = c;
+        if (t > 1) d.ctrl[t - 1].A = A;
+        if (q.newGoal != goalIdx) d.status->goalIdx = q.newGoal;
+    }
+}
+
+// 5 waves per SIMD: the 1 + nBlocks workgroups (1,025 at 262,144 slots) fit the chip at once.
+template <int AGENT, int OBS>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) void k_step(KgmtDev d, int t,
+                                                                                        int expand) {
+    extern __shared__ float4 sDyn[];   // [LDS obstacles][prefix: nBlocks + 1 ints]
+    __shared__ float sScore[kMaxR1];
+    __shared__ int sR1P[kMaxR1];
+    __shared__ uint32_t sSnap[kMaxR2Words];
+    __shared__ uint32_t sNew[kMaxR2Words];
+    __shared__ int sWaveCnt[kBlock / kWave];
+    __shared__ int sRed[2][kBlock / kWave];
+    __shared__ float sPart[8];
+    __shared__ int sCovInc[kMaxR1];
+
+    constexpr bool kLdsObs = (OBS == kObsLds || OBS == kObsLds4);
+    constexpr int kRegObs = obs_in_registers(OBS);
+    int* const sPfx = reinterpret_cast<int*>(sDyn + (kLdsObs ? d.nObs : 0));
+    if (blockIdx.x == 0) {
+        step_planner(d, t, expand, sPfx, sRed, sCovInc, sPart);
+        return;
+    }
+    float4* const sObs = sDyn;
+    const int tid = threadIdx.x;
+    const int lane = tid & (kWave - 1);
+    const int wave = tid >> 6;
+    const int b = (int)blockIdx.x - 1;   // this workgroup's 256-slot block
+    const int slot = b * kBlock + tid;
+    const int nW = d.nR2 >> 5;
+    const int pp = (t - 1) & 1, cp = t & 1;
+    unsigned long long* const pubCur = d.stepPub + (size_t)cp * (d.nR1 + nW);
+    long long* const tl = (d.timeline && t == d.timelineIter && expand)
+                              ? d.timeline + ((size_t)b * (kBlock / kWave) + wave) * kTimelineStamps
+                              : nullptr;
+    long long stamp[kTimelineStamps] = {0, 0, 0, 0, 0, 0, 0, 0};
+#define SBMP_STAMP(i)                                                                  \
+    do {                                                                               \
+        if (tl) stamp[i] = (long long)__builtin_amdgcn_s_memrealtime();                \
+    } while (0)
+    SBMP_STAMP(0);
+
+    // ---- loads that depend on nothing else (the control block as a plain load: a
+    // waiting scalar load would serialise behind the scan)
+    const int4 pk = *reinterpret_cast<const int4*>(d.stepCnt + (size_t)pp * kMaxStepBlocks + tid * 4);
+    const IterCtrl pc = d.ctrl[t - 1];
+    const int goalIdx = d.status->goalIdx;
+    const uint4 ra = d.rngA[slot];
+    const uint2 rb = d.rngB[slot];
+    const unsigned long long oldWord = (lane == 0) ? d.gnewOut[slot >> 6] : 0ull;
+    const float4 obsReg = (kLdsObs && tid < d.nObs) ? d.obstacles[tid] : make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int i = tid; i < d.nR1; i += kBlock) sR1P[i] = 0;
+    int A, jGoal;
+    step_scan(d, pk, sPfx, sRed, &A, &jGoal);
+    SBMP_STAMP(1);
+    const StepPlan q = step_plan(d, t, expand, pc, goalIdx, A, jGoal);
+    if (!q.ranPrev) return;
+
+    // ---- D6 clear of this block's words of t-1 (KGMT.cu:231,556)
+    const long long cleared = d.fixGNewClear ? (1ll << 62) : 32ll * q.grid;
+    unsigned long long word = oldWord;
+    if (lane == 0) {
+        const long long wbase = (long long)(slot >> 6) * kWave;
+        if (wbase + kWave <= cleared) word = 0ull;
+        else if (wbase < cleared) word = oldWord & ~((1ull << (cleared - wbase)) - 1ull);
+    }
+    const bool doExpand = q.executes && b * kBlock < q.H;
+    // ---- insert t-1: this block's flagged children (rows treeSize(t-1) + prefix +
+    // index).  Each entry carries its cost, so this is one load and three stores; an
+    // expanding block issues it right behind its parent loads (one round trip).
+    const int myPrev = sPfx[b + 1] - sPfx[b];
+    auto insert_prev = [&]() {
+        if (t > 1 && tid < myPrev) {
+            const int j = sPfx[b] + tid;
+            const int dst = q.tsPrev + j;
+            if (j < q.nIns && dst < d.M) {   // D13: the reference writes past M here
+                const float4* e =
+                    d.stepList + ((size_t)pp * d.nBlocks * kBlock + (size_t)b * kBlock + tid) * kStepEntry;
+                const float4 s4 = e[0];
+                const float4 u4 = e[1];
+                const float4 m4 = e[2];
+                d.treeState[dst] = s4;
+                d.treeCtrl[dst] = make_float4(u4.x, u4.y, u4.z, m4.x);   // cost = parent's + duration (KGMT.cu:631-633)
+                d.treeParent[dst] = __float_as_int(u4.w);
+            }
+        }
+    };
+    if (!doExpand) {
+        insert_prev();
+        if (lane == 0 && word != oldWord) d.gnewOut[slot >> 6] = word;
+        return;
+    }
+
+    // ---- expand t
+    const bool act = slot < q.S;
+    const int g = !act ? 0 : (q.k == 32) ? (slot >> 5) : div_small(slot, q.k);   // slot = g*k + i
+    const int parent = act ? q.gLo + g : 0;
+    const float4* src = d.treeState + parent;   // the parent's state, and its cost
+    const float* srcCost = &d.treeCtrl[parent].w;
+    if (parent >= q.tsPrev) {   // inserted by t-1: its block's compacted list
+        const int j = parent - q.tsPrev;
+        int lo = 0, hi = d.nBlocks;
+        while (hi - lo > 1) {
+            const int mid = (lo + hi) >> 1;
+            if (sPfx[mid] <= j) lo = mid;
+            else hi = mid;
+        }
+        src = d.stepList + ((size_t)pp * d.nBlocks * kBlock + (size_t)lo * kBlock + (j - sPfx[lo])) * kStepEntry;
+        srcCost = reinterpret_cast<const float*>(src + 2);
+    }
+    const float4 p = *src;
+    const float parentCost = *srcCost;
+    insert_prev();
+    float4 ro[kRegObs > 0 ? kRegObs : 1];
+#pragma unroll
+    for (int i = 0; i < kRegObs; ++i) ro[i] = d.obstacles[i];
+    if (kLdsObs) {
+        if (tid < d.nObs) sObs[tid] = obsReg;
+        for (int i = tid + kBlock; i < d.nObs; i += kBlock) sObs[i] = d.obstacles[i];
+        __syncthreads();
+    }
+    // The planner's scores and snapshot of t, prefetched (checked after propagation).
+    const bool pre = nW <= kStepPrefetch * kBlock;
+    unsigned long long pubS = 0ull, pubW[kStepPrefetch];
+    if (pre) {
+        if (tid < d.nR1) pubS = __hip_atomic_load(pubCur + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+        for (int j = 0; j < kStepPrefetch; ++j) {
+            pubW[j] = 0ull;
+            if (tid + j * kBlock < nW)
+                pubW[j] = __hip_atomic_load(pubCur + d.nR1 + tid + j * kBlock, __ATOMIC_RELAXED,
+                                            __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+    SBMP_STAMP(2);
+    const float4* obs = (kRegObs > 0) ? ro : kLdsObs ? sObs : d.obstacles;
+    Xorwow rs{ra.x, ra.y, ra.z, ra.w, rb.x, rb.y};
+    ChildOut out;
+    bool valid = false;
+    if (act) valid = (AGENT == 0) ? propagate_car<OBS>(p, rs, d, obs, out) : propagate_point<OBS>(p, rs, d, obs, out);
+    SBMP_STAMP(3);
+    {   // tags must read t; re-read (bounded) what the prefetch got too early
+        const unsigned want = (unsigned)t;
+        bool ok = pre;
+        if (pre) {
+            if (tid < d.nR1) {
+                ok &= (unsigned)(pubS >> 32) == want;
+                sScore[tid] = __uint_as_float((uint32_t)pubS);
+            }
+#pragma unroll
+            for (int j = 0; j < kStepPrefetch; ++j) {
+                const int w = tid + j * kBlock;
+                if (w < nW) {
+                    ok &= (unsigned)(pubW[j] >> 32) == want;
+                    sSnap[w] = (uint32_t)pubW[j];
+                    sNew[w] = 0u;
+                }
+            }
+        }
+        if (!__syncthreads_and(ok)) {
+            const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
+            bool late = false;
+            for (;;) {
+                ok = true;
+                if (tid < d.nR1) {
+                    const unsigned long long v = __hip_atomic_load(pubCur + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    ok &= (unsigned)(v >> 32) == want;
+                    sScore[tid] = __uint_as_float((uint32_t)v);
+                }
+                for (int w = tid; w < nW; w += kBlock) {
+                    const unsigned long long v =
+                        __hip_atomic_load(pubCur + d.nR1 + w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    ok &= (unsigned)(v >> 32) == want;
+                    sSnap[w] = (uint32_t)v;
+                    sNew[w] = 0u;
+                }
+                if (__syncthreads_and(ok)) break;
+                if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > 100000000ll) {   // 1 s: give up, report
+                    late = true;
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(8);
+            }
+            if (late && tid == 0) atomicExch(&d.status->error, 1);
+        }
+    }
+    SBMP_STAMP(4);
+    bool accept = false;
+    float4 cs = make_float4(0.f, 0.f, 0.f, 0.f), cc = cs;   // this slot's child (state, ctrl)
+    float cost = 0.0f;
+    if (act) {
+        const int q1 = getR1(out.state.x, out.state.y, d.R1Size, kN);   // N = 16 (KGMT.cu:8)
+        const int q2 = getR2(out.state.x, out.state.y, q1, d.R1Size, kN, d.R2Size, d.n);
+        if (valid) {
+            const float u = xorwow_uniform(rs);   // KGMT.cu:395
+            if (q2 >= 0) {
+                const uint32_t bit = 1u << (q2 & 31);
+                const bool r2Avail = sSnap[q2 >> 5] & bit;
+                accept = (u <= sScore[q1]) || !r2Avail;
+                if (!r2Avail) atomicOr(&sNew[q2 >> 5], bit);
+            }
+        }
+        cs = out.state;
+        cc = make_float4(out.a, out.steer, out.dur, __int_as_float(parent));
+        cost = parentCost + out.dur;   // getCost (KGMT.cu:631-633), as the insert computes it
+        d.uState[slot] = cs;
+        d.uCtrl[slot] = cc;
+        d.rngA[slot] = make_uint4(rs.v0, rs.v1, rs.v2, rs.v3);
+        d.rngB[slot] = make_uint2(rs.v4, rs.d);
+        if (q1 >= 0) atomicAdd(&sR1P[q1], valid ? 1 : 0x10000);
+        if (d.r2log) {
+            d.r2log[(size_t)(t % kFoldEvery) * d.logSlots + b * kBlock + tid] =
+                (q2 >= 0) ? (uint16_t)(q2 | (valid ? 0x8000 : 0)) : kNoKey;
+        } else if (q2 >= 0) {
+            atomicAdd(valid ? &d.R2Valid[q2] : &d.R2Invalid[q2], 1);
+        }
+    }
+    const unsigned long long mask = __ballot(accept);
+    const unsigned long long wordAll = __shfl(word, 0, kWave) | mask;   // GNew |= accept (stale bits survive)
+    const bool flagged = (wordAll >> lane) & 1ull;
+    if (flagged && !act) {   // a stale flag on a slot past S: the child last written there
+        cs = d.uState[slot];
+        cc = d.uCtrl[slot];
+        cost = d.treeCtrl[__float_as_int(cc.w)].w + cc.z;
+    }
+    bool inGoal = false;
+    if (flagged) {
+        const float dx = cs.x - d.goalX, dy = cs.y - d.goalY;   // inGoalRegion, KGMT.cu:635-638
+        inGoal = __builtin_sqrtf(dx * dx + dy * dy) < d.goalThreshold;
+    }
+    if (lane == 0) {
+        d.gnewOut[slot >> 6] = wordAll;
+        sWaveCnt[wave] = __popcll(wordAll);
+    }
+    __syncthreads();
+    SBMP_STAMP(5);
+    int idx = 0;
+    for (int i = 0; i < wave; ++i) idx += sWaveCnt[i];
+    const int cntB = sWaveCnt[0] + sWaveCnt[1] + sWaveCnt[2] + sWaveCnt[3];
+    idx += __popcll(wordAll & ((1ull << lane) - 1ull));
+    if (flagged) {
+        float4* e = d.stepList + ((size_t)cp * d.nBlocks * kBlock + (size_t)b * kBlock + idx) * kStepEntry;
+        e[0] = cs;
+        e[1] = cc;
+        e[2] = make_float4(cost, 0.0f, 0.0f, 0.0f);
+    }
+    int gl = (flagged && inGoal) ? idx : kNoGoalIdx;
+#pragma unroll
+    for (int off = kWave / 2; off > 0; off >>= 1) gl = min(gl, __shfl_xor(gl, off, kWave));
+    if (lane == 0) sRed[1][wave] = gl;
+    {   // one 64-bit atomic per touched cell, into this workgroup's replica
+        unsigned long long* const rep =
+            d.stepDelta + (size_t)(t % 3) * kDeltaReps * d.nR1 + (size_t)(b % kDeltaReps) * d.nR1;
+        for (int i = tid; i < d.nR1; i += kBlock) {
+            const int v = sR1P[i];
+            if (v) atomicAdd(&rep[i], (unsigned long long)(v & 0xffff) | ((unsigned long long)(v >> 16) << 32));
+        }
+    }
+    uint32_t* const newCur = d.stepR2New + (size_t)(t % 3) * nW;
+    for (int i = tid; i < nW; i += kBlock) {
+        const uint32_t w = sNew[i];
+        if (w) atomicOr(&newCur[i], w);
+    }
+    __syncthreads();
+    if (tid == 0) {
+        const int gmin2 = min(min(sRed[1][0], sRed[1][1]), min(sRed[1][2], sRed[1][3]));
+        d.stepCnt[(size_t)cp * kMaxStepBlocks + b] = cntB | ((gmin2 == kNoGoalIdx ? 0 : gmin2 + 1) << 16);
+    }
+    SBMP_STAMP(6);
+    if (tl) {
+        unsigned hw, xcc;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+        stamp[7] = ((long long)xcc << 32) | hw;
+    }
+    if (tl && lane == 0)
+        for (int i = 0; i < kTimelineStamps; ++i) tl[i] = stamp[i];
+#undef SBMP_STAMP
+}
+
 // ------------------------------------------------------------------ init
 __global__ void k_fill_i32(int* p, int v, long long n) {
     for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x)
@@ -828,6 +1364,7 @@ __global__ void k_seed_root(KgmtDev d, float4 rootState, float4 rootCtrl, int r1
         d.R1Cov[r2 / (d.n * d.n)] += 1;
     }
     d.status->goalIdx = kNoGoal;
+    d.status->error = 0;
 }
 
 // Export helpers: reference AoS layout.
@@ -925,6 +1462,41 @@ void launch_expand(const KgmtDev& d, int t, int agent, int blocks, int variant, 
                    const KernelTiming& tm) {
     if (agent == 0) launch_expand_agent<0>(d, t, blocks, variant, s, tm);
     else launch_expand_agent<1>(d, t, blocks, variant, s, tm);
+}
+
+template <int AGENT>
+static void launch_step_agent(const KgmtDev& d, int t, int expand, int variant, hipStream_t s,
+                              const KernelTiming& tm) {
+    const size_t pfx = sizeof(int) * ((size_t)d.nBlocks + 1);
+    const size_t shm = sizeof(float4) * (size_t)d.nObs + pfx;   // LDS obstacle forms
+    const dim3 grid(1 + d.nBlocks), block(kBlock);   // workgroup 0 plans, 1.. expand
+    if (d.gridStart) {
+        launch(k_step<AGENT, kObsGrid>, grid, block, pfx, s, tm, d, t, expand);
+    } else if (d.nObs > kMaxLdsObs) {
+        launch(k_step<AGENT, kObsGlobal>, grid, block, pfx, s, tm, d, t, expand);
+    } else if (d.nObs <= kMaxRegObs && (variant == 0 || variant == 3)) {
+        switch (d.nObs) {
+            case 0: launch(k_step<AGENT, kObsReg + 0>, grid, block, pfx, s, tm, d, t, expand); break;
+            case 1: launch(k_step<AGENT, kObsReg + 1>, grid, block, pfx, s, tm, d, t, expand); break;
+            case 2: launch(k_step<AGENT, kObsReg + 2>, grid, block, pfx, s, tm, d, t, expand); break;
+            case 3: launch(k_step<AGENT, kObsReg + 3>, grid, block, pfx, s, tm, d, t, expand); break;
+            case 4: launch(k_step<AGENT, kObsReg + 4>, grid, block, pfx, s, tm, d, t, expand); break;
+            case 5: launch(k_step<AGENT, kObsReg + 5>, grid, block, pfx, s, tm, d, t, expand); break;
+            case 6: launch(k_step<AGENT, kObsReg + 6>, grid, block, pfx, s, tm, d, t, expand); break;
+            case 7: launch(k_step<AGENT, kObsReg + 7>, grid, block, pfx, s, tm, d, t, expand); break;
+            default: launch(k_step<AGENT, kObsReg + 8>, grid, block, pfx, s, tm, d, t, expand); break;
+        }
+    } else if (variant == 2) {
+        launch(k_step<AGENT, kObsLds4>, grid, block, shm, s, tm, d, t, expand);
+    } else {
+        launch(k_step<AGENT, kObsLds>, grid, block, shm, s, tm, d, t, expand);
+    }
+}
+
+void launch_step(const KgmtDev& d, int t, int expand, int agent, int variant, hipStream_t s,
+                 const KernelTiming& tm) {
+    if (agent == 0) launch_step_agent<0>(d, t, expand, variant, s, tm);
+    else launch_step_agent<1>(d, t, expand, variant, s, tm);
 }
 
 void launch_fold_r2(const KgmtDev& d, int tFirst, int tLast, hipStream_t s, const KernelTiming& tm) {

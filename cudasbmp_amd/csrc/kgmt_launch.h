@@ -22,6 +22,9 @@ struct KernelTiming {
 void launch_expand(const KgmtDev& d, int t, int agent, int blocks, int variant, hipStream_t s,
                    const KernelTiming& tm = KernelTiming());
 // k_fold_r2: add the key log of iterations [tFirst, tLast] (at most kFoldEvery) to R2Valid / R2Invalid.
+// k_step(t): one launch per iteration on a single rank; expand == 0: flush pass.
+void launch_step(const KgmtDev& d, int t, int expand, int agent, int variant, hipStream_t s,
+                 const KernelTiming& tm = KernelTiming());
 void launch_fold_r2(const KgmtDev& d, int tFirst, int tLast, hipStream_t s, const KernelTiming& tm = KernelTiming());
 // k_finish(t): insert iteration t (insertBlocks = every global 256-slot block) +
 // prepare iteration t+1.  t = 0 prepares iteration 1 only (insertBlocks = 0).

@@ -113,12 +113,15 @@ KgmtPlanner::KgmtPlanner(const sbmp_kgmt_params& p, int nranks, int rank, Exchan
     d.uCtrl = alloc<float4>(slotsPadded_);
     d.rngA = alloc<uint4>(slotsPadded_);
     d.rngB = alloc<uint2>(slotsPadded_);
-    d.R1 = alloc<int>(d.nR1);
-    d.R1Avail = alloc<int>(d.nR1);
-    d.R1Valid = alloc<int>(d.nR1);
-    d.R1Invalid = alloc<int>(d.nR1);
-    d.R1Cov = alloc<int>(d.nR1);
-    d.R2Avail = alloc<uint32_t>(d.nR2 / 32);
+    {   // region tables [2 parities][R1, R1Avail, R1Valid, R1Invalid, R1Cov][nR1] (kgmt_device.h)
+        int* tab = alloc<int>((size_t)2 * 5 * d.nR1);
+        d.R1 = tab;
+        d.R1Avail = tab + d.nR1;
+        d.R1Valid = tab + 2 * d.nR1;
+        d.R1Invalid = tab + 3 * d.nR1;
+        d.R1Cov = tab + 4 * d.nR1;
+    }
+    d.R2Avail = alloc<uint32_t>((size_t)2 * (d.nR2 / 32));
     d.R2Snap = alloc<uint32_t>(d.nR2 / 32);
     d.R2Valid = alloc<int>(d.nR2);
     d.R2Invalid = alloc<int>(d.nR2);
@@ -171,6 +174,25 @@ KgmtPlanner::KgmtPlanner(const sbmp_kgmt_params& p, int nranks, int rank, Exchan
         views(xRecv_, false);
     }
     d.sharded = nranks > 1 || ex != nullptr;   // one RCCL rank still takes the sharded path
+    // One launch per iteration (k_step) on a single rank whose block prefix fits LDS;
+    // SBMP_STEP=0 keeps the two-kernel form (k_expand + k_finish).
+    d.stepMode = 0;
+    {
+        const char* v = getenv("SBMP_STEP");
+        if (!d.sharded && d.nBlocks <= kMaxStepBlocks && !(v && atoi(v) == 0)) d.stepMode = 1;
+    }
+    d.stepCnt = nullptr;
+    d.stepPub = nullptr;
+    d.stepList = nullptr;
+    d.stepDelta = nullptr;
+    d.stepR2New = nullptr;
+    if (d.stepMode) {
+        d.stepCnt = alloc<int>((size_t)2 * kMaxStepBlocks);
+        d.stepPub = alloc<unsigned long long>((size_t)2 * (d.nR1 + d.nR2 / 32));
+        d.stepList = alloc<float4>((size_t)2 * d.nBlocks * kBlock * kStepEntry);
+        d.stepDelta = alloc<unsigned long long>((size_t)3 * kDeltaReps * d.nR1);
+        d.stepR2New = alloc<uint32_t>((size_t)3 * (d.nR2 / 32));
+    }
     d.recCap = expandBlocks_ * kBlock;   // a rank never holds more flagged slots than it owns
     d.recOut = d.sharded ? alloc<float4>((size_t)2 * kRecordF4 * d.recCap) : nullptr;
     for (int q = 0; q < kMaxRanks; ++q) d.recPeer[q] = nullptr;
@@ -237,9 +259,14 @@ void KgmtPlanner::begin(const float* initial, const float* goal, const float* d_
     SBMP_HIP(hipMemsetAsync(xSend_, 0, sizeof(unsigned long long) * xWords_, s));
     if (local_) SBMP_HIP(hipMemsetAsync(local_, 0, sizeof(unsigned long long) * localWords_, s));
     if (xRecv_ != xSend_) SBMP_HIP(hipMemsetAsync(xRecv_, 0, sizeof(unsigned long long) * xWords_, s));
-    for (int* a : {d.R1, d.R1Avail, d.R1Valid, d.R1Invalid, d.R1Cov})
-        SBMP_HIP(hipMemsetAsync(a, 0, sizeof(int) * d.nR1, s));
-    SBMP_HIP(hipMemsetAsync(d.R2Avail, 0, sizeof(uint32_t) * (d.nR2 / 32), s));
+    SBMP_HIP(hipMemsetAsync(d.R1, 0, sizeof(int) * 2 * 5 * d.nR1, s));   // both parities
+    SBMP_HIP(hipMemsetAsync(d.R2Avail, 0, sizeof(uint32_t) * 2 * (d.nR2 / 32), s));
+    if (d.stepMode) {
+        SBMP_HIP(hipMemsetAsync(d.stepCnt, 0, sizeof(int) * 2 * kMaxStepBlocks, s));
+        SBMP_HIP(hipMemsetAsync(d.stepPub, 0, sizeof(unsigned long long) * 2 * (d.nR1 + d.nR2 / 32), s));
+        SBMP_HIP(hipMemsetAsync(d.stepDelta, 0, sizeof(unsigned long long) * 3 * kDeltaReps * d.nR1, s));
+        SBMP_HIP(hipMemsetAsync(d.stepR2New, 0, sizeof(uint32_t) * 3 * (d.nR2 / 32), s));
+    }
     SBMP_HIP(hipMemsetAsync(d.R2Snap, 0, sizeof(uint32_t) * (d.nR2 / 32), s));
     SBMP_HIP(hipMemsetAsync(d.R2Valid, 0, sizeof(int) * d.nR2, s));
     SBMP_HIP(hipMemsetAsync(d.R2Invalid, 0, sizeof(int) * d.nR2, s));
@@ -309,7 +336,8 @@ void KgmtPlanner::begin(const float* initial, const float* goal, const float* d_
     wallMs_ = 0.0;
     SBMP_HIP(hipStreamSynchronize(s));
     t0_ = now_ms();
-    launch_finish(d, 0, 0, s, timing(K_FINISH));   // prepares iteration 1
+    if (d.stepMode) flushed_ = false;   // k_step(1) plans iteration 1 itself
+    else launch_finish(d, 0, 0, s, timing(K_FINISH));   // prepares iteration 1
     SBMP_HIP(hipGetLastError());
 }
 
@@ -319,6 +347,12 @@ void KgmtPlanner::enqueue(int iterations) {
     for (int i = 0; i < iterations; ++i) {
         const int t = take_iteration();
         if (t == 0) break;
+        if (d_.stepMode) {
+            launch_step(d_, t, 1, p_.agent, expandVariant_, stream_, timing(K_STEP));
+            flushed_ = false;
+            stage_fold(t);
+            continue;
+        }
         stage_expand(t);
         if (d_.sharded) {
             stage_pack(t);
@@ -363,6 +397,10 @@ void KgmtPlanner::fold_to(int tLast) {
 }
 
 void KgmtPlanner::sync() {
+    if (d_.stepMode && begun_ && !flushed_) {   // complete the last iteration (insert, plan t_next)
+        launch_step(d_, t_next_, 0, p_.agent, expandVariant_, stream_, KernelTiming());
+        flushed_ = true;
+    }
     SBMP_HIP(hipStreamSynchronize(stream_));
     wallMs_ = now_ms() - t0_;
     if (d_.timeline && !timelineDumped_ && t_next_ > d_.timelineIter) {
@@ -407,6 +445,7 @@ bool KgmtPlanner::active() {
     PlannerStatus st;
     SBMP_HIP(hipMemcpy(&c, d_.ctrl + t_next_, sizeof(IterCtrl), hipMemcpyDeviceToHost));
     SBMP_HIP(hipMemcpy(&st, d_.status, sizeof(PlannerStatus), hipMemcpyDeviceToHost));
+    if (st.error) throw Error(SBMP_ERR_HIP, "k_step: the plan hand-off timed out");
     // ctrl[t_next] was written by the last enqueued plan kernel: it says whether the
     // next iteration would run (tree not full, limit not reached); the goal ends it too.
     return c.run && st.goalIdx == kNoGoal;
@@ -426,6 +465,7 @@ void KgmtPlanner::result(sbmp_plan_result* r) {
     std::vector<IterCtrl> c;
     PlannerStatus st;
     read_ctrl(c, st);
+    if (st.error) throw Error(SBMP_ERR_HIP, "k_step: the plan hand-off timed out");
     const int itr = last_executed(c);
     memset(r, 0, sizeof(*r));
     r->iterations = itr;
@@ -596,10 +636,12 @@ void KgmtPlanner::copy_regions(int* R1, int* R1Avail, int* R1Valid, int* R1Inval
     auto cp = [&](void* dst, const void* src, size_t bytes) {
         if (dst) SBMP_HIP(hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost));
     };
-    cp(R1, d_.R1, sizeof(int) * n1);
-    cp(R1Avail, d_.R1Avail, sizeof(int) * n1);
-    cp(R1Valid, d_.R1Valid, sizeof(int) * n1);
-    cp(R1Invalid, d_.R1Invalid, sizeof(int) * n1);
+    // k_step keeps the tables of iteration t_next (its flush pass planned it) at parity t_next & 1
+    const size_t tp = d_.stepMode ? (size_t)(t_next_ & 1) : 0;
+    cp(R1, d_.R1 + tp * 5 * n1, sizeof(int) * n1);
+    cp(R1Avail, d_.R1Avail + tp * 5 * n1, sizeof(int) * n1);
+    cp(R1Valid, d_.R1Valid + tp * 5 * n1, sizeof(int) * n1);
+    cp(R1Invalid, d_.R1Invalid + tp * 5 * n1, sizeof(int) * n1);
     cp(R1Score, d_.R1Score + (itr & 1) * n1, sizeof(float) * n1);
     if (ex_ && (R2Valid || R2Invalid)) {   // sharded: each rank folded its own children
         int* tmp = nullptr;
@@ -616,7 +658,8 @@ void KgmtPlanner::copy_regions(int* R1, int* R1Avail, int* R1Valid, int* R1Inval
     }
     if (R2Avail) {
         std::vector<uint32_t> bits(n2 / 32);
-        SBMP_HIP(hipMemcpy(bits.data(), d_.R2Avail, sizeof(uint32_t) * bits.size(), hipMemcpyDeviceToHost));
+        SBMP_HIP(hipMemcpy(bits.data(), d_.R2Avail + tp * (n2 / 32), sizeof(uint32_t) * bits.size(),
+                           hipMemcpyDeviceToHost));
         for (size_t i = 0; i < n2; ++i) R2Avail[i] = (bits[i >> 5] >> (i & 31)) & 1u;
     }
 }
@@ -721,7 +764,7 @@ void KgmtPlanner::collect_events() {
     pending_.clear();
 }
 
-static const char* kKernelNames[] = {"k_expand", "k_finish", "k_fold_r2", "k_pack"};
+static const char* kKernelNames[] = {"k_expand", "k_finish", "k_fold_r2", "k_pack", "k_step"};
 
 std::vector<float> KgmtPlanner::kernel_samples(const std::string& name) {
     collect_events();

@@ -131,7 +131,7 @@ public:
     int rank() const { return d_.rank; }
 
 private:
-    enum KernelId { K_EXPAND = 0, K_FINISH, K_FOLD, K_PACK, K_COUNT };
+    enum KernelId { K_EXPAND = 0, K_FINISH, K_FOLD, K_PACK, K_STEP, K_COUNT };
     KernelTiming timing(int id);
     void collect_events();
     void read_ctrl(std::vector<IterCtrl>& c, PlannerStatus& st);
@@ -150,6 +150,7 @@ private:
     int slotsPadded_ = 0, expandBlocks_ = 0, nbits_ = 1;
     int expandVariant_ = 0;   // SBMP_EXPAND_VARIANT: obstacle form, 0 = auto (3 if <= kMaxRegObs boxes, else 1)
     bool timelineDumped_ = false;
+    bool flushed_ = true;     // k_step mode: the last enqueued iteration has been inserted
     int lastFolded_ = 0;      // iterations <= lastFolded_ are in R2Valid / R2Invalid
     unsigned long long* local_ = nullptr;   // sharded: the owner's block counts + GNew words
     size_t localWords_ = 0;

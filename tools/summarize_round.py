@@ -44,8 +44,9 @@ def main():
     rows = list(csv.DictReader(open(glob.glob(os.path.join(trace_dir, "**", "*kernel_trace.csv"),
                                                 recursive=True)[0])))
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+    hot = "k_step" if any("k_step" in r["Kernel_Name"] for r in rows) else "k_expand"
     exp = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3 for r in rows
-           if "k_expand" in r["Kernel_Name"]]
+           if hot in r["Kernel_Name"]]
     W, K = bench["warmup"], bench["steps"]
     # bench.py: run A = W warm-up + K timed launches; run B (same seed) = W warm-up +
     # K event-stamped launches replaying the timed iterations.
@@ -54,7 +55,8 @@ def main():
     out = {name: {"launches": len(v), "mean_us": round(float(np.mean(v)), 3),
                   "median_us": round(float(np.median(v)), 3)} for name, v in win.items() if v}
     out["bench_roofline_avg_launch_us"] = bench["roofline"]["avg_launch_us"]
-    out["note"] = ("k_expand launches in trace order; the first 2W+2K belong to the bench planner "
+    out["kernel"] = hot
+    out["note"] = (f"{hot} launches in trace order (k_step: the flush passes before read-backs are launches too); the first 2W+2K belong to the bench planner "
                    "(the TTFS demo plans follow).  The bench's roofline divides algorithmic bytes by the mean of "
                    "its own dispatch-stamped HIP events over replay_timed (= the timed iterations).  Under "
                    "rocprofv3 those HIP events read high; compare the unprofiled bench line (bench.json).")
