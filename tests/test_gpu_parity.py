@@ -331,3 +331,29 @@ def test_solution_path_without_solution(d_obs, obstacles):
     assert len(rows) == 0 and samples.shape == (0, 7)
     rows, _, _ = g.solution_path(0)
     assert rows.tolist() == [0]
+
+
+@pytest.mark.parametrize("kw", [dict(), dict(fixGNewClear=True), dict(agent="point"),
+                                dict(samplesPerIteration=4096, batchRule="fill", maxTreeSize=100000,
+                                     numIterations=12, goalThreshold=0.0)])
+def test_two_kernel_form_bit_exact(kw, d_obs, obstacles, oracle_lib, monkeypatch):
+    """The two-launch form (k_expand + k_finish; sharded ranks and more than
+    kMaxStepBlocks blocks use it) forced on a single rank with SBMP_STEP=0."""
+    monkeypatch.setenv("SBMP_STEP", "0")
+    g, cfg, extra = _mk(**kw)
+    g.plan(DEMO_INITIAL, DEMO_GOAL, d_obs, len(obstacles), seed=17)
+    o = _oracle(cfg, extra)
+    o.plan(DEMO_INITIAL, DEMO_GOAL, obstacles, 17)
+    assert_same_state(g, o, label=f"two-kernel {kw}")
+
+
+def test_more_blocks_than_the_step_kernel_holds(d_obs, obstacles, oracle_lib):
+    """300,000 slots = 1,172 blocks > kMaxStepBlocks: the planner falls back to the
+    two-launch form on its own."""
+    g, cfg, extra = _mk(samplesPerIteration=300000, maxTreeSize=700000, numIterations=3, goalThreshold=0.0,
+                        batchRule="fill")
+    g.plan(DEMO_INITIAL, DEMO_GOAL, d_obs, len(obstacles), seed=8)
+    o = _oracle(cfg, extra, threads=16)
+    o.plan(DEMO_INITIAL, DEMO_GOAL, obstacles, 8)
+    assert g.iter_log()[:, 5].max() > 262144
+    assert_same_state(g, o, label="1172 blocks")
