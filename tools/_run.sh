@@ -1,4 +1,7 @@
-set -e
-timeout -k 10 900 python3 -m pytest tests -x -q -m gpu > gpurun_out/gpu_step.log 2>&1
-for i in 1 2; do timeout -k 10 200 python3 bench.py --no-cpu-baseline --no-ttfs >> gpurun_out/b7.json 2>>gpurun_out/b7.err; done
-SBMP_TIMELINE_ITER=45 SBMP_TIMELINE_OUT=gpurun_out/tls5.bin timeout -k 10 200 python3 bench.py --no-cpu-baseline --no-ttfs > /dev/null 2>&1
+mkdir -p gpurun_out
+timeout -k 10 400 python3 -u -m pytest tests -q -m gpu --timeout 120 --timeout-method thread -p no:cacheprovider > gpurun_out/gpu_tests.log 2>&1
+grep -E "passed|failed|FAILED" gpurun_out/gpu_tests.log | tail -20
+for rep in 1 2; do for w in 0 3 7 1; do
+  SBMP_WT=$w timeout -k 10 200 python3 bench.py --no-cpu-baseline --no-ttfs > gpurun_out/b_w${w}_$rep.json 2> gpurun_out/b_w${w}_$rep.err || { echo "bench $w rc=$?"; exit 1; }
+  python3 -c "import json;d=json.loads(open('gpurun_out/b_w${w}_$rep.json').read().splitlines()[-1]);print('wt',$w,d['value']/1e9,d['ms_per_step']*1e3,d['roofline']['achieved'])"
+done; done

@@ -13,6 +13,9 @@ import sys
 import numpy as np
 
 NAMES = ["entry", "prologue", "propagate", "accept+store", "count_regions", "barrier", "flush"]
+# k_step (SBMP_STEP=1, the default on one rank): 1 after the count scan, 2 after the
+# parent/insert/prefetch loads are issued, 3 after propagation, 4 after the hand-off check
+STEP_NAMES = ["entry", "scan", "issued", "propagate", "handoff", "barrier", "end"]
 
 
 FIN_PLAN = ["entry", "prefix", "deltas", "r2new", "cov", "scores", "R1Score", "end"]
@@ -38,10 +41,17 @@ def finish(path):
 
 
 def main():
+    global NAMES
     if sys.argv[1].endswith(".fin"):
         finish(sys.argv[1])
         return
     a = np.fromfile(sys.argv[1], dtype=np.int64).reshape(-1, 8)
+    if "--step" in sys.argv:   # k_step: the planner's entry / publish stamps are in <out>.fin[0:2]
+        NAMES = STEP_NAMES
+        f = np.fromfile(sys.argv[1] + ".fin", dtype=np.int64)
+        t0w = a[a[:, 6] != 0, 0].min()
+        print(f"planner: entry {(f[0] - t0w) / 100.0:+.2f} us, publish {(f[1] - t0w) / 100.0:+.2f} us "
+              f"(relative to the first expanding wave's entry)")
     live = a[a[:, 6] != 0]
     print(f"{len(a)} waves, {len(live)} ran the full path")
     t0 = live[:, 0].min()
