@@ -158,38 +158,7 @@ struct KgmtDev {
     long long* timeline;
     long long* timelineFin;   // k_finish(timelineIter): [1 + nBlocks][kTimelineStamps], wave 0 of each workgroup
     int timelineIter;
-    // Write-through (sc1) stores for k_step's per-slot outputs, bit mask (SBMP_WT):
-    // 1 = child (uState/uCtrl), 2 = XORWOW state, 4 = compacted entries.  A kernel
-    // boundary writes back every dirty L2 line (B / 6 TB/s, MI355X_MICROARCH.md
-    // "boundary"); write-through stores move that traffic into the waves' own time.
-    int wt;
 };
-
-// 16-B / 8-B stores with sc1: written through to memory, line dropped from this XCD's L2.
-// A VMEM store of more than 8 B reads its data VGPRs one cycle after issue, and the
-// compiler's hazard recognizer does not see stores inside inline asm: without the
-// s_nop the next VALU may overwrite the data first (seen on MI355X as the store's
-// first 8 bytes replaced by the next store's address).
-typedef uint32_t sbmp_u32x4 __attribute__((ext_vector_type(4)));
-typedef uint32_t sbmp_u32x2 __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ void store_wt(void* p, sbmp_u32x4 v) {
-    asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" : : "v"(p), "v"(v) : "memory");
-}
-__device__ __forceinline__ void store_wt(float4* p, float4 v) {
-    store_wt(static_cast<void*>(p), sbmp_u32x4{__float_as_uint(v.x), __float_as_uint(v.y), __float_as_uint(v.z),
-                                               __float_as_uint(v.w)});
-}
-__device__ __forceinline__ void store_wt(uint4* p, uint4 v) {
-    store_wt(static_cast<void*>(p), sbmp_u32x4{v.x, v.y, v.z, v.w});
-}
-__device__ __forceinline__ void store_wt(uint2* p, uint2 v) {
-    asm volatile("global_store_dwordx2 %0, %1, off sc1" : : "v"(p), "v"(sbmp_u32x2{v.x, v.y}) : "memory");
-}
-template <typename T>
-__device__ __forceinline__ void store_sel(T* p, T v, bool wt) {
-    if (wt) store_wt(p, v);
-    else *p = v;
-}
 
 // ---------------------------------------------------------------- grid binning
 // reference KGMT.cu:602-609 / 610-629.  Float->int truncates toward zero; an
@@ -356,16 +325,13 @@ __device__ __forceinline__ void sincos_quadrant(float r, int q, float* s, float*
     *c = u2f(f2u(c0) ^ ((uint32_t)((q + 1) & 2) << 30));
 }
 
-// PH = false: the caller has proven |x| <= 105615 for every lane (wave_cull's theta
-// bound), so the branch and the registers of the Payne-Hanek path are not emitted.
-template <bool PH = true>
 __device__ __forceinline__ void sincos_pred(float x, float* s, float* c) {
     const float j = __builtin_rintf(x * 0.636619772f);
     float r = __builtin_fmaf(j, -1.57079601e+00f, x);
     r = __builtin_fmaf(j, -3.13916473e-07f, r);
     r = __builtin_fmaf(j, -5.39030253e-15f, r);
     sincos_quadrant(r, (int)j, s, c);
-    if (PH && !(__builtin_fabsf(x) <= 105615.0f)) {   // rare: huge, inf or NaN argument
+    if (!(__builtin_fabsf(x) <= 105615.0f)) {   // rare: huge, inf or NaN argument
         if (finitef(x)) {
             int q;
             const float rh = reduce_payne_hanek(x, &q);
@@ -414,34 +380,6 @@ __device__ __forceinline__ bool motion_valid_culled(float minx, float miny, floa
     return !hit;
 }
 
-// The controls of one child depend only on its slot's XORWOW stream, not on the
-// parent: k_step draws them while its parent row is still in flight.
-struct Controls {
-    float a, steer, dur, dt, tanS;   // point agent: a = vx, steer = vy; tanS unused
-};
-
-// reference statePropagator.cu:16-20 (car) / the point agent's (vx, vy, duration).
-// Same operation sequence as the oracle (D9-D11): fmaf where nvcc would contract,
-// steering via one double fma.
-template <int AGENT>
-__device__ __forceinline__ Controls draw_controls(Xorwow& rs, const KgmtDev& d) {
-    Controls c;
-    if (AGENT == 0) {
-        c.a = __builtin_fmaf(xorwow_uniform(rs), 10.0f, -5.0f);
-        const float u2 = xorwow_uniform(rs);
-        c.steer = (float)__builtin_fma((double)(u2 * 2.0f), 3.141592653589793, -3.141592653589793);
-        c.dur = __builtin_fmaf(xorwow_uniform(rs), 1.0f, 0.05f);
-        c.tanS = tanf_d(c.steer);
-    } else {
-        c.a = __builtin_fmaf(xorwow_uniform(rs), 2.0f, -1.0f);
-        c.steer = __builtin_fmaf(xorwow_uniform(rs), 2.0f, -1.0f);
-        c.dur = __builtin_fmaf(xorwow_uniform(rs), 1.0f, 0.05f);
-        c.tanS = 0.0f;
-    }
-    c.dt = c.dur / (float)d.numDisc;
-    return c;
-}
-
 // reference statePropagator.cu:5-76 (car).  Same operation sequence as the oracle
 // (D9-D11): fmaf where nvcc would contract, steering via one double fma.
 // v / agentLength: when agentLength is a power of two, v * (1/agentLength) is the
@@ -452,14 +390,26 @@ __device__ __forceinline__ Controls draw_controls(Xorwow& rs, const KgmtDev& d) 
 // (theta, v), a lane that fails the collision test keeps all four (exactly the
 // state at the reference's break), and later steps leave a dead lane unchanged.
 // The wave leaves the loop once no lane is alive.
-template <int OBS, bool PH>
-__device__ __forceinline__ bool car_steps(float& x, float& y, float& theta, float& v, const Controls& ctl,
-                                          const KgmtDev& d, const float4* obs, const WaveCull& cull) {
-    const float a = ctl.a, dt = ctl.dt, tan_steering = ctl.tanS;
+template <int OBS>
+__device__ __forceinline__ bool propagate_car(float4 p, Xorwow& rs, const KgmtDev& d, const float4* obs,
+                                              ChildOut& out) {
+    const float a = __builtin_fmaf(xorwow_uniform(rs), 10.0f, -5.0f);
+    const float u2 = xorwow_uniform(rs);
+    const float steering = (float)__builtin_fma((double)(u2 * 2.0f), 3.141592653589793, -3.141592653589793);
+    const float duration = __builtin_fmaf(xorwow_uniform(rs), 1.0f, 0.05f);
+    const float dt = duration / (float)d.numDisc;
+    float x = p.x, y = p.y, theta = p.z, v = p.w;
+    const float tan_steering = tanf_d(steering);
+    // |v| <= |v0| + |a| t, so the displacement stays below T |v0| + |a| T^2 / 2.
+    WaveCull cull{~0u, true};
+    if (OBS >= kObsReg) {
+        const float r = duration * __builtin_fabsf(p.w) + 0.5f * __builtin_fabsf(a) * duration * duration;
+        cull = wave_cull<OBS>(p.x, p.y, r, r, obs, d);
+    }
     bool alive = true;
     for (int i = 0; i < d.numDisc; ++i) {
         float st, ct;
-        sincos_pred<PH>(theta, &st, &ct);
+        sincos_pred(theta, &st, &ct);
         const float nx = __builtin_fmaf(v * ct, dt, x);
         const float ny = __builtin_fmaf(v * st, dt, y);
         const bool oob = cull.bounds && ((nx <= 0.0f) | (nx >= d.width) | (ny <= 0.0f) | (ny >= d.height));
@@ -485,28 +435,6 @@ __device__ __forceinline__ bool car_steps(float& x, float& y, float& theta, floa
         alive = adv & freeSeg;
         if (__ballot(alive) == 0ull) break;
     }
-    return alive;
-}
-
-template <int OBS>
-__device__ __forceinline__ bool integrate_car(float4 p, const Controls& ctl, const KgmtDev& d, const float4* obs,
-                                              ChildOut& out) {
-    const float a = ctl.a, steering = ctl.steer, duration = ctl.dur, dt = ctl.dt, tan_steering = ctl.tanS;
-    float x = p.x, y = p.y, theta = p.z, v = p.w;
-    // |v| <= |v0| + |a| t, so the displacement stays below T |v0| + |a| T^2 / 2.
-    WaveCull cull{~0u, true};
-    if (OBS >= kObsReg) {
-        const float r = duration * __builtin_fabsf(p.w) + 0.5f * __builtin_fabsf(a) * duration * duration;
-        cull = wave_cull<OBS>(p.x, p.y, r, r, obs, d);
-    }
-    // |theta| grows by at most |v| |tan delta| / L per unit time, |v| <= |v0| + |a| t:
-    // if no lane can leave the Cody-Waite range, the steps omit the Payne-Hanek path.
-    const float Lr = (d.invAgentLength != 0.0f) ? d.invAgentLength : 1.0f / d.agentLength;
-    const float thMax = __builtin_fabsf(p.z) + duration * __builtin_fabsf(tan_steering) * __builtin_fabsf(Lr) *
-                                                   (__builtin_fabsf(p.w) + __builtin_fabsf(a) * duration);
-    const bool alive = (__ballot(!(thMax * 1.01f + 1.0f <= 100000.0f)) == 0ull)
-                           ? car_steps<OBS, false>(x, y, theta, v, ctl, d, obs, cull)
-                           : car_steps<OBS, true>(x, y, theta, v, ctl, d, obs, cull);
     out.state = make_float4(x, y, theta, v);
     out.a = a;
     out.steer = steering;
@@ -516,9 +444,12 @@ __device__ __forceinline__ bool integrate_car(float4 p, const Controls& ctl, con
 
 // Holonomic R2 point (build extension), predicated like propagate_car.
 template <int OBS>
-__device__ __forceinline__ bool integrate_point(float4 p, const Controls& ctl, const KgmtDev& d, const float4* obs,
+__device__ __forceinline__ bool propagate_point(float4 p, Xorwow& rs, const KgmtDev& d, const float4* obs,
                                                 ChildOut& out) {
-    const float vx = ctl.a, vy = ctl.steer, duration = ctl.dur, dt = ctl.dt;
+    const float vx = __builtin_fmaf(xorwow_uniform(rs), 2.0f, -1.0f);
+    const float vy = __builtin_fmaf(xorwow_uniform(rs), 2.0f, -1.0f);
+    const float duration = __builtin_fmaf(xorwow_uniform(rs), 1.0f, 0.05f);
+    const float dt = duration / (float)d.numDisc;
     float x = p.x, y = p.y;
     WaveCull cull{~0u, true};
     if (OBS >= kObsReg)
@@ -546,18 +477,6 @@ __device__ __forceinline__ bool integrate_point(float4 p, const Controls& ctl, c
     out.steer = vy;
     out.dur = duration;
     return alive;
-}
-
-template <int AGENT, int OBS>
-__device__ __forceinline__ bool integrate(float4 p, const Controls& c, const KgmtDev& d, const float4* obs,
-                                          ChildOut& out) {
-    return (AGENT == 0) ? integrate_car<OBS>(p, c, d, obs, out) : integrate_point<OBS>(p, c, d, obs, out);
-}
-
-template <int AGENT, int OBS>
-__device__ __forceinline__ bool propagate(float4 p, Xorwow& rs, const KgmtDev& d, const float4* obs, ChildOut& out) {
-    const Controls c = draw_controls<AGENT>(rs, d);
-    return integrate<AGENT, OBS>(p, c, d, obs, out);
 }
 
 }  // namespace sbmp

@@ -191,7 +191,8 @@ __global__ __launch_bounds__(kBlock) void k_expand(KgmtDev d, int t) {
     if (act) {
         Xorwow rs{ra.x, ra.y, ra.z, ra.w, rb.x, rb.y};
         ChildOut out;
-        const bool valid = propagate<AGENT, OBS>(p, rs, d, obs, out);
+        const bool valid = (AGENT == 0) ? propagate_car<OBS>(p, rs, d, obs, out)
+                                        : propagate_point<OBS>(p, rs, d, obs, out);
         SBMP_STAMP(2);
         const int r1 = getR1(out.state.x, out.state.y, d.R1Size, kN);   // N = 16 (KGMT.cu:8)
         const int r2 = getR2(out.state.x, out.state.y, r1, d.R1Size, kN, d.R2Size, d.n);
@@ -837,18 +838,8 @@ struct StepPlan {
     int tsPrev, treeSize, gLo, H, grid, nIns, newGoal, runT, nG, k, nExp, S;
     bool executes;
 };
-
-// What iteration t needs of t-1's plan: ctrl[t-1] and the goal status, read when the
-// launch starts (every workgroup derives the same values).
-struct StepCarry {
-    int executed, treeSize, gLo, nExp, H, goalIdx;
-};
-__device__ __forceinline__ StepCarry carry_from(const IterCtrl& pc, int goalIdx) {
-    return StepCarry{pc.executed, pc.treeSize, pc.gLo, pc.nExp, pc.H, goalIdx};
-}
-
-__device__ __forceinline__ StepPlan step_plan(const KgmtDev& d, int t, int expand, const StepCarry& pc, int A,
-                                              int jGoal) {
+__device__ __forceinline__ StepPlan step_plan(const KgmtDev& d, int t, int expand, const IterCtrl& pc, int goalIdx,
+                                              int A, int jGoal) {
     StepPlan q;
     q.ranPrev = (t == 1) || pc.executed;
     q.tsPrev = (t == 1) ? 1 : pc.treeSize;
@@ -859,7 +850,7 @@ __device__ __forceinline__ StepPlan step_plan(const KgmtDev& d, int t, int expan
     q.nIns = 32 * q.grid < A ? 32 * q.grid : A;
     // The lowest inserted row of t-1 inside the goal radius (D4): rows grow with j,
     // so if the lowest candidate is not inserted (D13) none is.
-    q.newGoal = pc.goalIdx;
+    q.newGoal = goalIdx;
     if (jGoal < q.nIns && (long long)q.tsPrev + jGoal < d.M) q.newGoal = min(q.newGoal, q.tsPrev + jGoal);
     q.runT = (t <= d.numIterations) && (q.treeSize < d.M);   // KGMT.cu:118,255
     q.nG = 0;
@@ -875,28 +866,13 @@ __device__ __forceinline__ StepPlan step_plan(const KgmtDev& d, int t, int expan
     return q;
 }
 
-__device__ __forceinline__ StepCarry carry_next(const StepPlan& q) {
-    return StepCarry{q.executes ? 1 : 0, q.treeSize, q.gLo, q.nExp, q.H, q.newGoal};
-}
-
-struct StepLds {
-    float sScore[kMaxR1];
-    int sR1P[kMaxR1];
-    uint32_t sSnap[kMaxR2Words];
-    uint32_t sNew[kMaxR2Words];
-    int sWaveCnt[kBlock / kWave];
-    int sRed[2][kBlock / kWave];
-    float sPart[8];
-    int sCovInc[kMaxR1];
-};
-
 // Workgroup 0 of k_step(t): tables of t (R1 deltas folded, R2New merged into R2Avail
 // = the snapshot, R1Cov), scores (updateR1, KGMT.cu:485-538, CUB order D8), ctrl[t];
-// scores and snapshot published as 8-B words tagged with t.  Returns whether
-// iteration t executes.
-__device__ __forceinline__ bool step_planner(const KgmtDev& d, int t, int expand, StepCarry& cr, int* sPfx,
-                                             StepLds& L, int tid) {
+// scores and snapshot published as 8-B words tagged with t.
+__device__ __forceinline__ void step_planner(const KgmtDev& d, int t, int expand, int* sPfx,
+                                             int (*sRed)[kBlock / kWave], int* sCovInc, float* sPart) {
     constexpr int kW = kMaxR2Words / kBlock;
+    const int tid = threadIdx.x;
     const int nW = d.nR2 >> 5;
     const int nn = d.n * d.n;
     const int pp = (t - 1) & 1, cp = t & 1;
@@ -906,6 +882,8 @@ __device__ __forceinline__ bool step_planner(const KgmtDev& d, int t, int expand
     if (tl) d.timelineFin[0] = (long long)__builtin_amdgcn_s_memrealtime();
     // every input at entry
     const int4 pk = *reinterpret_cast<const int4*>(d.stepCnt + (size_t)pp * kMaxStepBlocks + tid * 4);
+    const IterCtrl pc = d.ctrl[t - 1];
+    const int goalIdx = d.status->goalIdx;
     const int* tabPrev = d.R1 + (size_t)pp * 5 * d.nR1;
     int r1 = tabPrev[cell], r1a = tabPrev[d.nR1 + cell], r1v = tabPrev[2 * d.nR1 + cell],
         r1i = tabPrev[3 * d.nR1 + cell], r1c = tabPrev[4 * d.nR1 + cell];
@@ -922,12 +900,10 @@ __device__ __forceinline__ bool step_planner(const KgmtDev& d, int t, int expand
         availW[j] = availPrev[w];
         newW[j] = newPrev[w];
     }
-    for (int i = tid; i < d.nR1; i += kBlock) L.sCovInc[i] = 0;
+    for (int i = tid; i < d.nR1; i += kBlock) sCovInc[i] = 0;
     int A, jGoal;
-    step_scan(d, pk, sPfx, L.sRed, &A, &jGoal);
-    const StepCarry pc = cr;
-    const StepPlan q = step_plan(d, t, expand, pc, A, jGoal);
-    cr = carry_next(q);
+    step_scan(d, pk, sPfx, sRed, &A, &jGoal);
+    const StepPlan q = step_plan(d, t, expand, pc, goalIdx, A, jGoal);
     int* tabCur = d.R1 + (size_t)cp * 5 * d.nR1;
     if (!q.ranPrev) {   // t-1 did not run: the loop has ended; carry the tables forward
         for (int i = tid; i < 5 * d.nR1; i += kBlock) tabCur[i] = tabPrev[i];
@@ -938,7 +914,7 @@ __device__ __forceinline__ bool step_planner(const KgmtDev& d, int t, int expand
             c.H = pc.H;
             d.ctrl[t] = c;
         }
-        return false;
+        return;
     }
     const int nv = (int)(dl & 0xffffffffull), ni = (int)(dl >> 32);
     r1 += nv + ni;      // KGMT.cu:392
@@ -954,19 +930,19 @@ __device__ __forceinline__ bool step_planner(const KgmtDev& d, int t, int expand
             const uint32_t fresh = newW[j] & ~availW[j];
             snapW[j] = availW[j] | newW[j];   // R2Avail of t = the snapshot (D2)
             if (fresh && nn % 32 == 0) {
-                atomicAdd(&L.sCovInc[(32 * w) / nn], __popc(fresh));
+                atomicAdd(&sCovInc[(32 * w) / nn], __popc(fresh));
             } else {
                 uint32_t f = fresh;
                 while (f) {
                     const int b = __builtin_ctz(f);
                     f &= f - 1u;
-                    atomicAdd(&L.sCovInc[(32 * w + b) / nn], 1);
+                    atomicAdd(&sCovInc[(32 * w + b) / nn], 1);
                 }
             }
         }
     }
     __syncthreads();
-    r1c += L.sCovInc[cell];
+    r1c += sCovInc[cell];
     float scv = 1.0f;
     if (q.runT) {
         float sc = 0.0f;
@@ -985,11 +961,11 @@ __device__ __forceinline__ bool step_planner(const KgmtDev& d, int t, int expand
             const float o = __shfl_down(v, off, 32);
             v = v + o;
         }
-        if ((tid & 31) == 0) L.sPart[tid >> 5] = v;
+        if ((tid & 31) == 0) sPart[tid >> 5] = v;
         __syncthreads();
-        float total = L.sPart[0];
+        float total = sPart[0];
 #pragma unroll
-        for (int w = 1; w < 8; ++w) total = total + L.sPart[w];
+        for (int w = 1; w < 8; ++w) total = total + sPart[w];
         scv = (r1a == 0) ? 1.0f : sc / total;
     }
     // publish first (tagged 8-B words, written through)
@@ -1040,20 +1016,36 @@ __device__ __forceinline__ bool step_planner(const KgmtDev& d, int t, int expand
         for (int i = 0; i < 5; ++i) c.pad[i] = 0;
         d.ctrl[t] = c;
         if (t > 1) d.ctrl[t - 1].A = A;
-        if (q.newGoal != pc.goalIdx) d.status->goalIdx = q.newGoal;
+        if (q.newGoal != goalIdx) d.status->goalIdx = q.newGoal;
     }
-    return q.executes;
 }
 
-// Workgroups 1..nBlocks of k_step(t): block b = its 256 slots.  Returns whether iteration t executed (the same answer in every
-// workgroup).
+// 5 waves per SIMD: the 1 + nBlocks workgroups (1,025 at 262,144 slots) fit the chip at once.
 template <int AGENT, int OBS>
-__device__ __forceinline__ bool step_expander(const KgmtDev& d, int t, int expand, int b, StepCarry& cr, int* sPfx,
-                                              float4* sObs, StepLds& L, int tid) {
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) void k_step(KgmtDev d, int t,
+                                                                                        int expand) {
+    extern __shared__ float4 sDyn[];   // [LDS obstacles][prefix: nBlocks + 1 ints]
+    __shared__ float sScore[kMaxR1];
+    __shared__ int sR1P[kMaxR1];
+    __shared__ uint32_t sSnap[kMaxR2Words];
+    __shared__ uint32_t sNew[kMaxR2Words];
+    __shared__ int sWaveCnt[kBlock / kWave];
+    __shared__ int sRed[2][kBlock / kWave];
+    __shared__ float sPart[8];
+    __shared__ int sCovInc[kMaxR1];
+
     constexpr bool kLdsObs = (OBS == kObsLds || OBS == kObsLds4);
     constexpr int kRegObs = obs_in_registers(OBS);
+    int* const sPfx = reinterpret_cast<int*>(sDyn + (kLdsObs ? d.nObs : 0));
+    if (blockIdx.x == 0) {
+        step_planner(d, t, expand, sPfx, sRed, sCovInc, sPart);
+        return;
+    }
+    float4* const sObs = sDyn;
+    const int tid = threadIdx.x;
     const int lane = tid & (kWave - 1);
     const int wave = tid >> 6;
+    const int b = (int)blockIdx.x - 1;   // this workgroup's 256-slot block
     const int slot = b * kBlock + tid;
     const int nW = d.nR2 >> 5;
     const int pp = (t - 1) & 1, cp = t & 1;
@@ -1068,25 +1060,21 @@ __device__ __forceinline__ bool step_expander(const KgmtDev& d, int t, int expan
     } while (0)
     SBMP_STAMP(0);
 
-    // ---- loads that depend on nothing else.  The XORWOW state goes first: the
-    // controls are drawn from it while the counts are in flight (vmcnt is in order,
-    // so a load issued behind the counts would wait for them too).
+    // ---- loads that depend on nothing else (the control block as a plain load: a
+    // waiting scalar load would serialise behind the scan)
+    const int4 pk = *reinterpret_cast<const int4*>(d.stepCnt + (size_t)pp * kMaxStepBlocks + tid * 4);
+    const IterCtrl pc = d.ctrl[t - 1];
+    const int goalIdx = d.status->goalIdx;
     const uint4 ra = d.rngA[slot];
     const uint2 rb = d.rngB[slot];
-    const int4 pk = *reinterpret_cast<const int4*>(d.stepCnt + (size_t)pp * kMaxStepBlocks + tid * 4);
     const unsigned long long oldWord = (lane == 0) ? d.gnewOut[slot >> 6] : 0ull;
     const float4 obsReg = (kLdsObs && tid < d.nObs) ? d.obstacles[tid] : make_float4(0.f, 0.f, 0.f, 0.f);
-    for (int i = tid; i < d.nR1; i += kBlock) L.sR1P[i] = 0;
-    // Controls of this slot's child (statePropagator.cu:16-20): they depend only on the
-    // stream, which advances only where the slot is active (its state is stored then).
-    Xorwow rs{ra.x, ra.y, ra.z, ra.w, rb.x, rb.y};
-    const Controls ctl = draw_controls<AGENT>(rs, d);
+    for (int i = tid; i < d.nR1; i += kBlock) sR1P[i] = 0;
     int A, jGoal;
-    step_scan(d, pk, sPfx, L.sRed, &A, &jGoal);
+    step_scan(d, pk, sPfx, sRed, &A, &jGoal);
     SBMP_STAMP(1);
-    const StepPlan q = step_plan(d, t, expand, cr, A, jGoal);
-    cr = carry_next(q);
-    if (!q.ranPrev) return false;
+    const StepPlan q = step_plan(d, t, expand, pc, goalIdx, A, jGoal);
+    if (!q.ranPrev) return;
 
     // ---- D6 clear of this block's words of t-1 (KGMT.cu:231,556)
     const long long cleared = d.fixGNewClear ? (1ll << 62) : 32ll * q.grid;
@@ -1120,7 +1108,7 @@ __device__ __forceinline__ bool step_expander(const KgmtDev& d, int t, int expan
     if (!doExpand) {
         insert_prev();
         if (lane == 0 && word != oldWord) d.gnewOut[slot >> 6] = word;
-        return q.executes;
+        return;
     }
 
     // ---- expand t
@@ -1166,9 +1154,10 @@ __device__ __forceinline__ bool step_expander(const KgmtDev& d, int t, int expan
     }
     SBMP_STAMP(2);
     const float4* obs = (kRegObs > 0) ? ro : kLdsObs ? sObs : d.obstacles;
+    Xorwow rs{ra.x, ra.y, ra.z, ra.w, rb.x, rb.y};
     ChildOut out;
     bool valid = false;
-    if (act) valid = integrate<AGENT, OBS>(p, ctl, d, obs, out);
+    if (act) valid = (AGENT == 0) ? propagate_car<OBS>(p, rs, d, obs, out) : propagate_point<OBS>(p, rs, d, obs, out);
     SBMP_STAMP(3);
     {   // tags must read t; re-read (bounded) what the prefetch got too early
         const unsigned want = (unsigned)t;
@@ -1176,15 +1165,15 @@ __device__ __forceinline__ bool step_expander(const KgmtDev& d, int t, int expan
         if (pre) {
             if (tid < d.nR1) {
                 ok &= (unsigned)(pubS >> 32) == want;
-                L.sScore[tid] = __uint_as_float((uint32_t)pubS);
+                sScore[tid] = __uint_as_float((uint32_t)pubS);
             }
 #pragma unroll
             for (int j = 0; j < kStepPrefetch; ++j) {
                 const int w = tid + j * kBlock;
                 if (w < nW) {
                     ok &= (unsigned)(pubW[j] >> 32) == want;
-                    L.sSnap[w] = (uint32_t)pubW[j];
-                    L.sNew[w] = 0u;
+                    sSnap[w] = (uint32_t)pubW[j];
+                    sNew[w] = 0u;
                 }
             }
         }
@@ -1196,14 +1185,14 @@ __device__ __forceinline__ bool step_expander(const KgmtDev& d, int t, int expan
                 if (tid < d.nR1) {
                     const unsigned long long v = __hip_atomic_load(pubCur + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     ok &= (unsigned)(v >> 32) == want;
-                    L.sScore[tid] = __uint_as_float((uint32_t)v);
+                    sScore[tid] = __uint_as_float((uint32_t)v);
                 }
                 for (int w = tid; w < nW; w += kBlock) {
                     const unsigned long long v =
                         __hip_atomic_load(pubCur + d.nR1 + w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     ok &= (unsigned)(v >> 32) == want;
-                    L.sSnap[w] = (uint32_t)v;
-                    L.sNew[w] = 0u;
+                    sSnap[w] = (uint32_t)v;
+                    sNew[w] = 0u;
                 }
                 if (__syncthreads_and(ok)) break;
                 if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > 100000000ll) {   // 1 s: give up, report
@@ -1226,19 +1215,19 @@ __device__ __forceinline__ bool step_expander(const KgmtDev& d, int t, int expan
             const float u = xorwow_uniform(rs);   // KGMT.cu:395
             if (q2 >= 0) {
                 const uint32_t bit = 1u << (q2 & 31);
-                const bool r2Avail = L.sSnap[q2 >> 5] & bit;
-                accept = (u <= L.sScore[q1]) || !r2Avail;
-                if (!r2Avail) atomicOr(&L.sNew[q2 >> 5], bit);
+                const bool r2Avail = sSnap[q2 >> 5] & bit;
+                accept = (u <= sScore[q1]) || !r2Avail;
+                if (!r2Avail) atomicOr(&sNew[q2 >> 5], bit);
             }
         }
         cs = out.state;
         cc = make_float4(out.a, out.steer, out.dur, __int_as_float(parent));
         cost = parentCost + out.dur;   // getCost (KGMT.cu:631-633), as the insert computes it
-        store_sel(d.uState + slot, cs, d.wt & 1);
-        store_sel(d.uCtrl + slot, cc, d.wt & 1);
-        store_sel(d.rngA + slot, make_uint4(rs.v0, rs.v1, rs.v2, rs.v3), d.wt & 2);
-        store_sel(d.rngB + slot, make_uint2(rs.v4, rs.d), d.wt & 2);
-        if (q1 >= 0) atomicAdd(&L.sR1P[q1], valid ? 1 : 0x10000);
+        d.uState[slot] = cs;
+        d.uCtrl[slot] = cc;
+        d.rngA[slot] = make_uint4(rs.v0, rs.v1, rs.v2, rs.v3);
+        d.rngB[slot] = make_uint2(rs.v4, rs.d);
+        if (q1 >= 0) atomicAdd(&sR1P[q1], valid ? 1 : 0x10000);
         if (d.r2log) {
             d.r2log[(size_t)(t % kFoldEvery) * d.logSlots + b * kBlock + tid] =
                 (q2 >= 0) ? (uint16_t)(q2 | (valid ? 0x8000 : 0)) : kNoKey;
@@ -1261,41 +1250,40 @@ __device__ __forceinline__ bool step_expander(const KgmtDev& d, int t, int expan
     }
     if (lane == 0) {
         d.gnewOut[slot >> 6] = wordAll;
-        L.sWaveCnt[wave] = __popcll(wordAll);
+        sWaveCnt[wave] = __popcll(wordAll);
     }
     __syncthreads();
     SBMP_STAMP(5);
     int idx = 0;
-    for (int i = 0; i < wave; ++i) idx += L.sWaveCnt[i];
-    const int cntB = L.sWaveCnt[0] + L.sWaveCnt[1] + L.sWaveCnt[2] + L.sWaveCnt[3];
+    for (int i = 0; i < wave; ++i) idx += sWaveCnt[i];
+    const int cntB = sWaveCnt[0] + sWaveCnt[1] + sWaveCnt[2] + sWaveCnt[3];
     idx += __popcll(wordAll & ((1ull << lane) - 1ull));
     if (flagged) {
         float4* e = d.stepList + ((size_t)cp * d.nBlocks * kBlock + (size_t)b * kBlock + idx) * kStepEntry;
-        const bool wt = d.wt & 4;
-        store_sel(e, cs, wt);
-        store_sel(e + 1, cc, wt);
-        store_sel(e + 2, make_float4(cost, 0.0f, 0.0f, 0.0f), wt);
+        e[0] = cs;
+        e[1] = cc;
+        e[2] = make_float4(cost, 0.0f, 0.0f, 0.0f);
     }
     int gl = (flagged && inGoal) ? idx : kNoGoalIdx;
 #pragma unroll
     for (int off = kWave / 2; off > 0; off >>= 1) gl = min(gl, __shfl_xor(gl, off, kWave));
-    if (lane == 0) L.sRed[1][wave] = gl;
+    if (lane == 0) sRed[1][wave] = gl;
     {   // one 64-bit atomic per touched cell, into this workgroup's replica
         unsigned long long* const rep =
             d.stepDelta + (size_t)(t % 3) * kDeltaReps * d.nR1 + (size_t)(b % kDeltaReps) * d.nR1;
         for (int i = tid; i < d.nR1; i += kBlock) {
-            const int v = L.sR1P[i];
+            const int v = sR1P[i];
             if (v) atomicAdd(&rep[i], (unsigned long long)(v & 0xffff) | ((unsigned long long)(v >> 16) << 32));
         }
     }
     uint32_t* const newCur = d.stepR2New + (size_t)(t % 3) * nW;
     for (int i = tid; i < nW; i += kBlock) {
-        const uint32_t w = L.sNew[i];
+        const uint32_t w = sNew[i];
         if (w) atomicOr(&newCur[i], w);
     }
     __syncthreads();
     if (tid == 0) {
-        const int gmin2 = min(min(L.sRed[1][0], L.sRed[1][1]), min(L.sRed[1][2], L.sRed[1][3]));
+        const int gmin2 = min(min(sRed[1][0], sRed[1][1]), min(sRed[1][2], sRed[1][3]));
         d.stepCnt[(size_t)cp * kMaxStepBlocks + b] = cntB | ((gmin2 == kNoGoalIdx ? 0 : gmin2 + 1) << 16);
     }
     SBMP_STAMP(6);
@@ -1308,20 +1296,6 @@ __device__ __forceinline__ bool step_expander(const KgmtDev& d, int t, int expan
     if (tl && lane == 0)
         for (int i = 0; i < kTimelineStamps; ++i) tl[i] = stamp[i];
 #undef SBMP_STAMP
-    return true;
-}
-
-// 5 waves per SIMD: the 1 + nBlocks workgroups (1,025 at 262,144 slots) fit the chip at once.
-template <int AGENT, int OBS>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) void k_step(KgmtDev d, int t,
-                                                                                        int expand) {
-    extern __shared__ float4 sDyn[];   // [LDS obstacles][prefix: nBlocks + 1 ints]
-    __shared__ StepLds L;
-    constexpr bool kLdsObs = (OBS == kObsLds || OBS == kObsLds4);
-    int* const sPfx = reinterpret_cast<int*>(sDyn + (kLdsObs ? d.nObs : 0));
-    StepCarry cr = carry_from(d.ctrl[t - 1], d.status->goalIdx);
-    if (blockIdx.x == 0) step_planner(d, t, expand, cr, sPfx, L, (int)threadIdx.x);
-    else step_expander<AGENT, OBS>(d, t, expand, (int)blockIdx.x - 1, cr, sPfx, sDyn, L, (int)threadIdx.x);
 }
 
 // ------------------------------------------------------------------ init

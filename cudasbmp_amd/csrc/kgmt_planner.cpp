@@ -181,8 +181,6 @@ KgmtPlanner::KgmtPlanner(const sbmp_kgmt_params& p, int nranks, int rank, Exchan
         const char* v = getenv("SBMP_STEP");
         if (!d.sharded && d.nBlocks <= kMaxStepBlocks && !(v && atoi(v) == 0)) d.stepMode = 1;
     }
-    d.wt = 0;
-    if (const char* v = getenv("SBMP_WT")) d.wt = atoi(v) & 7;
     d.stepCnt = nullptr;
     d.stepPub = nullptr;
     d.stepList = nullptr;

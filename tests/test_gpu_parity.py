@@ -358,16 +358,3 @@ def test_more_blocks_than_the_step_kernel_holds(d_obs, obstacles, oracle_lib):
     assert g.iter_log()[:, 5].max() > 262144
     assert_same_state(g, o, label="1172 blocks")
 
-
-@pytest.mark.parametrize("kw", [dict(), dict(fixGNewClear=True), dict(agent="point"),
-                                dict(samplesPerIteration=4096, batchRule="fill", maxTreeSize=100000,
-                                     numIterations=12, goalThreshold=0.0)])
-def test_write_through_stores_bit_exact(kw, d_obs, obstacles, oracle_lib, monkeypatch):
-    """One launch per iteration (k_step) with write-through slot stores (SBMP_WT=7:
-    child, XORWOW state and compacted entries stored with sc1)."""
-    monkeypatch.setenv("SBMP_WT", "7")
-    g, cfg, extra = _mk(**kw)
-    g.plan(DEMO_INITIAL, DEMO_GOAL, d_obs, len(obstacles), seed=17)
-    o = _oracle(cfg, extra)
-    o.plan(DEMO_INITIAL, DEMO_GOAL, obstacles, 17)
-    assert_same_state(g, o, label=f"write-through {kw}")

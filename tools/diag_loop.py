@@ -1,6 +1,6 @@
 """Diagnostic: stepwise demo plan against the oracle, printing the first differing
 rows / columns of each array (used to bisect kernel-form differences, e.g.
-SBMP_STEP=2 python tools/diag_loop.py)."""
+SBMP_STEP=0 python tools/diag_loop.py)."""
 import os
 import sys
 
