@@ -74,6 +74,10 @@ constexpr int kDeltaReps = 8;
 constexpr int kMaxStepBlocks = 1024;   // k_step: one int4 of block counts per thread (<= 262,144 slots)
 constexpr int kNoGoalIdx = 0x7fffffff;
 constexpr int kStepEntry = 3;       // k_step list entry: state, (a, steer, dur, parent), (cost, -, -, -)
+// k_step: when iteration t-1 accepted at most this many children, the planner
+// workgroup (idle once it has published) writes all of them into the tree, and the
+// expanding workgroups issue no insert loads or stores ahead of their propagation.
+constexpr int kPlannerInsertMax = 4096;
 constexpr int kStepPrefetch = 2;    // snapshot words per thread prefetched before propagation (nR2 <= 16,384)
 constexpr int kInsertBase = 8;   // k_finish workgroup of insert block 0 (one per XCD ahead of it)
 constexpr int kRecordF4 = 3;   // sharded record: state, ctrl (a, steer, dur, parent), (block, index in block, -, -)
@@ -159,6 +163,27 @@ struct KgmtDev {
     long long* timelineFin;   // k_finish(timelineIter): [1 + nBlocks][kTimelineStamps], wave 0 of each workgroup
     int timelineIter;
 };
+
+// 16-B / 8-B stores with sc1: written through to memory during the kernel, so the
+// dependent kernel boundary has fewer dirty L2 lines to write back (MI355X_MICROARCH.md,
+// "boundary": + dirty bytes / 6 TB/s).  A VMEM store of more than 8 B reads its data
+// VGPRs after issue and the hazard recognizer does not see stores inside inline asm:
+// the s_nop keeps the next VALU from overwriting the data first.
+typedef uint32_t sbmp_u32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t sbmp_u32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void store_wt(void* p, sbmp_u32x4 v) {
+    asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" : : "v"(p), "v"(v) : "memory");
+}
+__device__ __forceinline__ void store_wt(float4* p, float4 v) {
+    store_wt(static_cast<void*>(p), sbmp_u32x4{__float_as_uint(v.x), __float_as_uint(v.y), __float_as_uint(v.z),
+                                               __float_as_uint(v.w)});
+}
+__device__ __forceinline__ void store_wt(uint4* p, uint4 v) {
+    store_wt(static_cast<void*>(p), sbmp_u32x4{v.x, v.y, v.z, v.w});
+}
+__device__ __forceinline__ void store_wt(uint2* p, uint2 v) {
+    asm volatile("global_store_dwordx2 %0, %1, off sc1" : : "v"(p), "v"(sbmp_u32x2{v.x, v.y}) : "memory");
+}
 
 // ---------------------------------------------------------------- grid binning
 // reference KGMT.cu:602-609 / 610-629.  Float->int truncates toward zero; an

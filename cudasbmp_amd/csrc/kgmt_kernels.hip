@@ -205,10 +205,10 @@ __global__ __launch_bounds__(kBlock) void k_expand(KgmtDev d, int t) {
                 if (!r2Avail) atomicOr(&sNew[r2 >> 5], bit);
             }
         }
-        d.uState[slot] = out.state;
-        d.uCtrl[slot] = make_float4(out.a, out.steer, out.dur, __int_as_float(parent));
-        d.rngA[slot] = make_uint4(rs.v0, rs.v1, rs.v2, rs.v3);
-        d.rngB[slot] = make_uint2(rs.v4, rs.d);
+        store_wt(d.uState + slot, out.state);   // write-through: fewer dirty lines at the boundary
+        store_wt(d.uCtrl + slot, make_float4(out.a, out.steer, out.dur, __int_as_float(parent)));
+        store_wt(d.rngA + slot, make_uint4(rs.v0, rs.v1, rs.v2, rs.v3));
+        store_wt(d.rngB + slot, make_uint2(rs.v4, rs.d));
         if (r1 >= 0) atomicAdd(&sR1P[r1], valid ? 1 : 0x10000);
         if (d.r2log) {
             d.r2log[(size_t)(t % kFoldEvery) * d.logSlots + (int)blockIdx.x * kBlock + tid] =
@@ -1018,6 +1018,35 @@ __device__ __forceinline__ void step_planner(const KgmtDev& d, int t, int expand
         if (t > 1) d.ctrl[t - 1].A = A;
         if (q.newGoal != goalIdx) d.status->goalIdx = q.newGoal;
     }
+    // Insert t-1's flagged children (rows tsPrev + j, KGMT.cu:540-593) when they are
+    // few: everything above is what the expanders wait for, and from here on this
+    // workgroup is idle.
+    if (t > 1 && A <= kPlannerInsertMax) {
+        const int n = min(q.nIns, d.M - q.tsPrev);   // D13: the reference writes past M
+        const float4* listPrev = d.stepList + (size_t)pp * d.nBlocks * kBlock * kStepEntry;
+        // list entry of row j: block lo with sPfx[lo] <= j < sPfx[lo + 1]
+        auto entry = [&](int j) {
+            int lo = 0;
+            for (int step = kMaxStepBlocks / 2; step > 0; step >>= 1)
+                if (lo + step < d.nBlocks && sPfx[lo + step] <= j) lo += step;
+            return listPrev + ((size_t)lo * kBlock + (j - sPfx[lo])) * kStepEntry;
+        };
+        auto put = [&](int j, float4 s4, float4 u4, float c) {
+            const int dst = q.tsPrev + j;
+            d.treeState[dst] = s4;
+            d.treeCtrl[dst] = make_float4(u4.x, u4.y, u4.z, c);   // cost = parent's + duration (KGMT.cu:631-633)
+            d.treeParent[dst] = __float_as_int(u4.w);
+        };
+        for (int j0 = tid; j0 < n; j0 += 2 * kBlock) {   // two rows per thread per round, loads first
+            const int j1 = j0 + kBlock;
+            const float4* e0 = entry(j0);
+            const float4* e1 = entry(min(j1, n - 1));
+            const float4 s0 = e0[0], u0 = e0[1], s1 = e1[0], u1 = e1[1];
+            const float c0 = e0[2].x, c1 = e1[2].x;
+            put(j0, s0, u0, c0);
+            if (j1 < n) put(j1, s1, u1, c1);
+        }
+    }
 }
 
 // 5 waves per SIMD: the 1 + nBlocks workgroups (1,025 at 262,144 slots) fit the chip at once.
@@ -1089,8 +1118,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) voi
     // index).  Each entry carries its cost, so this is one load and three stores; an
     // expanding block issues it right behind its parent loads (one round trip).
     const int myPrev = sPfx[b + 1] - sPfx[b];
+    const bool selfInsert = A > kPlannerInsertMax;   // else the planner workgroup inserts
     auto insert_prev = [&]() {
-        if (t > 1 && tid < myPrev) {
+        if (t > 1 && selfInsert && tid < myPrev) {
             const int j = sPfx[b] + tid;
             const int dst = q.tsPrev + j;
             if (j < q.nIns && dst < d.M) {   // D13: the reference writes past M here
@@ -1128,29 +1158,29 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) voi
         src = d.stepList + ((size_t)pp * d.nBlocks * kBlock + (size_t)lo * kBlock + (j - sPfx[lo])) * kStepEntry;
         srcCost = reinterpret_cast<const float*>(src + 2);
     }
+    // Parent, obstacles and the planner's published scores and snapshot of t (checked
+    // after propagation) are issued back to back and waited for together.  The
+    // prefetch addresses are clamped instead of predicated: a load under a divergent
+    // branch makes the wait ahead of propagation a full vmcnt(0).
     const float4 p = *src;
     const float parentCost = *srcCost;
-    insert_prev();
     float4 ro[kRegObs > 0 ? kRegObs : 1];
 #pragma unroll
     for (int i = 0; i < kRegObs; ++i) ro[i] = d.obstacles[i];
+    const bool pre = nW <= kStepPrefetch * kBlock;
+    unsigned long long pubS = 0ull, pubW[kStepPrefetch];
+    if (pre) {
+        pubS = __hip_atomic_load(pubCur + min(tid, d.nR1 - 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+        for (int j = 0; j < kStepPrefetch; ++j)
+            pubW[j] = __hip_atomic_load(pubCur + d.nR1 + min(tid + j * kBlock, nW - 1), __ATOMIC_RELAXED,
+                                        __HIP_MEMORY_SCOPE_AGENT);
+    }
+    insert_prev();
     if (kLdsObs) {
         if (tid < d.nObs) sObs[tid] = obsReg;
         for (int i = tid + kBlock; i < d.nObs; i += kBlock) sObs[i] = d.obstacles[i];
         __syncthreads();
-    }
-    // The planner's scores and snapshot of t, prefetched (checked after propagation).
-    const bool pre = nW <= kStepPrefetch * kBlock;
-    unsigned long long pubS = 0ull, pubW[kStepPrefetch];
-    if (pre) {
-        if (tid < d.nR1) pubS = __hip_atomic_load(pubCur + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#pragma unroll
-        for (int j = 0; j < kStepPrefetch; ++j) {
-            pubW[j] = 0ull;
-            if (tid + j * kBlock < nW)
-                pubW[j] = __hip_atomic_load(pubCur + d.nR1 + tid + j * kBlock, __ATOMIC_RELAXED,
-                                            __HIP_MEMORY_SCOPE_AGENT);
-        }
     }
     SBMP_STAMP(2);
     const float4* obs = (kRegObs > 0) ? ro : kLdsObs ? sObs : d.obstacles;
@@ -1223,10 +1253,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) voi
         cs = out.state;
         cc = make_float4(out.a, out.steer, out.dur, __int_as_float(parent));
         cost = parentCost + out.dur;   // getCost (KGMT.cu:631-633), as the insert computes it
-        d.uState[slot] = cs;
-        d.uCtrl[slot] = cc;
-        d.rngA[slot] = make_uint4(rs.v0, rs.v1, rs.v2, rs.v3);
-        d.rngB[slot] = make_uint2(rs.v4, rs.d);
+        store_wt(d.uState + slot, cs);   // write-through: fewer dirty lines at the boundary
+        store_wt(d.uCtrl + slot, cc);
+        store_wt(d.rngA + slot, make_uint4(rs.v0, rs.v1, rs.v2, rs.v3));
+        store_wt(d.rngB + slot, make_uint2(rs.v4, rs.d));
         if (q1 >= 0) atomicAdd(&sR1P[q1], valid ? 1 : 0x10000);
         if (d.r2log) {
             d.r2log[(size_t)(t % kFoldEvery) * d.logSlots + b * kBlock + tid] =
