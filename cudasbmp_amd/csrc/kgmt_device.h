@@ -185,6 +185,25 @@ __device__ __forceinline__ void store_wt(uint2* p, uint2 v) {
     asm volatile("global_store_dwordx2 %0, %1, off sc1" : : "v"(p), "v"(sbmp_u32x2{v.x, v.y}) : "memory");
 }
 
+// Inclusive prefix sum over the 64 lanes of a wave with DPP: shifts by 1, 2, 4, 8
+// inside each 16-lane row, then the row totals by row_bcast:15 / row_bcast:31.  Every
+// lane must be active.  (__shfl_up compiles to ds_bpermute, one LDS round trip per step.)
+__device__ __forceinline__ int wave_incl_sum(int v) {
+    v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, false);   // row_shr:1
+    v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, false);   // row_shr:2
+    v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xf, false);   // row_shr:4
+    v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xf, 0xf, false);   // row_shr:8
+    v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xa, 0xf, false);   // row_bcast:15 -> rows 1, 3
+    v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xc, 0xf, false);   // row_bcast:31 -> rows 2, 3
+    return v;
+}
+
+// Value of v in the lowest lane where `pick` holds (`fallback` if none); uniform.
+__device__ __forceinline__ int first_lane_value(bool pick, int v, int fallback) {
+    const unsigned long long m = __ballot(pick);
+    return m ? __builtin_amdgcn_readlane(v, (int)__builtin_ctzll(m)) : fallback;
+}
+
 // ---------------------------------------------------------------- grid binning
 // reference KGMT.cu:602-609 / 610-629.  Float->int truncates toward zero; an
 // out-of-int-range or NaN quotient maps to -1 (D3).

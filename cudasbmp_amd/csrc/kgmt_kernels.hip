@@ -804,28 +804,24 @@ __device__ __forceinline__ void step_scan(const KgmtDev& d, int4 pk, int* sPfx, 
         gl4[e] = g;
         run += c;
     }
-    int incl = run;
-#pragma unroll
-    for (int off = 1; off < kWave; off <<= 1) {
-        const int o = __shfl_up(incl, off, kWave);
-        if (lane >= off) incl += o;
-    }
+    const int incl = wave_incl_sum(run);
     if (lane == kWave - 1) sRed[0][wave] = incl;
     __syncthreads();
     int base = incl - run;
     for (int w = 0; w < wave; ++w) base += sRed[0][w];
     *A = sRed[0][0] + sRed[0][1] + sRed[0][2] + sRed[0][3];
+    // Prefixes grow with g and a goal child's in-block index is below its block's
+    // count, so the lowest g holding a goal child has the lowest global index.
     int gmin = kNoGoalIdx;
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
+    for (int e = 3; e >= 0; --e) {
         const int g = tid * 4 + e;
         const int pf = base + loc[e];
         if (g <= d.nBlocks) sPfx[g] = pf;
-        if (gl4[e] >= 0) gmin = min(gmin, pf + gl4[e]);
+        if (gl4[e] >= 0) gmin = pf + gl4[e];
     }
     if (tid == kBlock - 1 && d.nBlocks == kMaxStepBlocks) sPfx[kMaxStepBlocks] = *A;
-#pragma unroll
-    for (int off = kWave / 2; off > 0; off >>= 1) gmin = min(gmin, __shfl_xor(gmin, off, kWave));
+    gmin = first_lane_value(gmin != kNoGoalIdx, gmin, kNoGoalIdx);
     if (lane == 0) sRed[1][wave] = gmin;
     __syncthreads();
     *jGoal = min(min(sRed[1][0], sRed[1][1]), min(sRed[1][2], sRed[1][3]));
@@ -1147,16 +1143,39 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) voi
     const int parent = act ? q.gLo + g : 0;
     const float4* src = d.treeState + parent;   // the parent's state, and its cost
     const float* srcCost = &d.treeCtrl[parent].w;
-    if (parent >= q.tsPrev) {   // inserted by t-1: its block's compacted list
-        const int j = parent - q.tsPrev;
-        int lo = 0, hi = d.nBlocks;
-        while (hi - lo > 1) {
-            const int mid = (lo + hi) >> 1;
-            if (sPfx[mid] <= j) lo = mid;
-            else hi = mid;
+    // A parent inserted by t-1 is read from its block's compacted list: block lo with
+    // sPfx[lo] <= j < sPfx[lo + 1].  j grows with the lane; when a wave's parents are
+    // at most two consecutive list positions jA, jB (k >= 32 children per parent) both
+    // are found by a two-level 32-ary ballot search (lanes 0-31 for jA, 32-63 for jB):
+    // two dependent LDS reads instead of log2(nBlocks).
+    const bool fromList = parent >= q.tsPrev;
+    const int j = parent - q.tsPrev;
+    const unsigned long long need = __ballot(fromList);
+    if (need) {
+        const int jA = __builtin_amdgcn_readlane(j, (int)__builtin_ctzll(need));
+        const int jB = __builtin_amdgcn_readlane(j, 63 - (int)__builtin_clzll(need));
+        int lo = 0;
+        if (jB - jA <= 1) {
+            const int jj = (lane < 32) ? jA : jB;
+            const int sub = lane & 31;
+            int idx = sub * 32;
+            unsigned long long m = __ballot((idx < d.nBlocks ? sPfx[idx] : INT_MAX) <= jj);
+            const int cA = __popcll(m & 0xffffffffull) - 1, cB = __popcll(m >> 32) - 1;
+            idx = ((lane < 32) ? cA : cB) * 32 + sub;
+            m = __ballot((idx < d.nBlocks ? sPfx[idx] : INT_MAX) <= jj);
+            lo = (j == jA) ? cA * 32 + __popcll(m & 0xffffffffull) - 1 : cB * 32 + __popcll(m >> 32) - 1;
+        } else {
+            int hi = d.nBlocks;
+            while (hi - lo > 1) {
+                const int mid = (lo + hi) >> 1;
+                if (sPfx[mid] <= j) lo = mid;
+                else hi = mid;
+            }
         }
-        src = d.stepList + ((size_t)pp * d.nBlocks * kBlock + (size_t)lo * kBlock + (j - sPfx[lo])) * kStepEntry;
-        srcCost = reinterpret_cast<const float*>(src + 2);
+        if (fromList) {
+            src = d.stepList + ((size_t)pp * d.nBlocks * kBlock + (size_t)lo * kBlock + (j - sPfx[lo])) * kStepEntry;
+            srcCost = reinterpret_cast<const float*>(src + 2);
+        }
     }
     // Parent, obstacles and the planner's published scores and snapshot of t (checked
     // after propagation) are issued back to back and waited for together.  The
@@ -1266,7 +1285,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) voi
         }
     }
     const unsigned long long mask = __ballot(accept);
-    const unsigned long long wordAll = __shfl(word, 0, kWave) | mask;   // GNew |= accept (stale bits survive)
+    const unsigned long long word0 =   // lane 0's word
+        ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)(word >> 32), 0) << 32) |
+        (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)word, 0);
+    const unsigned long long wordAll = word0 | mask;   // GNew |= accept (stale bits survive)
     const bool flagged = (wordAll >> lane) & 1ull;
     if (flagged && !act) {   // a stale flag on a slot past S: the child last written there
         cs = d.uState[slot];
@@ -1294,9 +1316,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) voi
         e[1] = cc;
         e[2] = make_float4(cost, 0.0f, 0.0f, 0.0f);
     }
-    int gl = (flagged && inGoal) ? idx : kNoGoalIdx;
-#pragma unroll
-    for (int off = kWave / 2; off > 0; off >>= 1) gl = min(gl, __shfl_xor(gl, off, kWave));
+    // idx grows with the lane: the first goal child is the wave's lowest
+    const int gl = first_lane_value(flagged && inGoal, idx, kNoGoalIdx);
     if (lane == 0) sRed[1][wave] = gl;
     {   // one 64-bit atomic per touched cell, into this workgroup's replica
         unsigned long long* const rep =
