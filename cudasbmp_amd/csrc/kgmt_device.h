@@ -79,6 +79,7 @@ constexpr int kStepEntry = 3;       // k_step list entry: state, (a, steer, dur,
 // expanding workgroups issue no insert loads or stores ahead of their propagation.
 constexpr int kPlannerInsertMax = 4096;
 constexpr int kStepPrefetch = 2;    // snapshot words per thread prefetched before propagation (nR2 <= 16,384)
+static_assert(kBlock / kWave == 4 && kMaxR1 == kBlock, "the flush and prefix code assumes 4 waves and 256 R1 cells");
 constexpr int kInsertBase = 8;   // k_finish workgroup of insert block 0 (one per XCD ahead of it)
 constexpr int kRecordF4 = 3;   // sharded record: state, ctrl (a, steer, dur, parent), (block, index in block, -, -)
 
@@ -88,6 +89,8 @@ struct KgmtDev {
     int batchRule;        // 0 = reference rule (+ cap), 1 = fill the cap (D14)
     int nranks, rank;
     float width, height, agentLength, invAgentLength, goalThreshold, R1Size, R2Size, goalX, goalY;
+    // RN(1/b) for div_by when the host verified it for this b (planner.cpp markstein_rcp), else 0
+    float rcpR1Size, rcpR2Size, rcpNumDisc, rcpAgentLength;
     float4* treeState;
     float4* treeCtrl;
     int* treeParent;
@@ -228,6 +231,45 @@ SBMP_HD int getR2(float x, float y, int r1, float R1Size, int N, float R2Size, i
     bool okx, oky;
     const int cx = cell_of(lx / R2Size, &okx);
     const int cy = cell_of(ly / R2Size, &oky);
+    return (okx && oky && cx >= 0 && cx < n && cy >= 0 && cy < n) ? r1 * (n * n) + cy * n + cx : -1;
+}
+
+// a / b for a per-plan constant b, given y = RN(1/b) computed on the host (Markstein):
+// q0 = RN(a y), r = a - q0 b exactly by FMA, RN(q0 + r y) = RN(a / b) while r stays
+// normal.  tools/check_fast_division.c checks every float a for the divisors the
+// tests and the bench use: bit-exact for |a| >= 2^-100, and the truncation to a grid
+// cell agrees for every a.  3 VALU instead of the ~11 of an IEEE division.
+__device__ __forceinline__ float div_by(float a, float b, float y) {
+    const float q0 = a * y;
+    const float r = __builtin_fmaf(-q0, b, a);
+    return __builtin_fmaf(r, y, q0);
+}
+
+// y == 0: the host could not verify div_by for this b; the branch is uniform.
+__device__ __forceinline__ float div_or_ieee(float a, float b, float y) {
+    if (y != 0.0f) return div_by(a, b, y);
+    return a / b;
+}
+
+// getR1 / getR2 of the kernels: the same cells as the SBMP_HD forms above (they only
+// truncate the quotients), with the divisions by R1Size / R2Size as div_by.
+__device__ __forceinline__ int getR1_k(float x, float y, float R1Size, float rcpR1, int N) {
+    bool okx, oky;
+    const int cx = cell_of(div_or_ieee(x, R1Size, rcpR1), &okx);
+    const int cy = cell_of(div_or_ieee(y, R1Size, rcpR1), &oky);
+    return (okx && oky && cx >= 0 && cx < N && cy >= 0 && cy < N) ? cy * N + cx : -1;
+}
+
+__device__ __forceinline__ int getR2_k(float x, float y, int r1, float R1Size, int N, float R2Size, float rcpR2,
+                                       int n) {
+    if (r1 < 0) return -1;
+    const int cyR1 = r1 / N;
+    const int cxR1 = r1 % N;
+    const float lx = x - (float)cxR1 * R1Size;
+    const float ly = y - (float)cyR1 * R1Size;
+    bool okx, oky;
+    const int cx = cell_of(div_or_ieee(lx, R2Size, rcpR2), &okx);
+    const int cy = cell_of(div_or_ieee(ly, R2Size, rcpR2), &oky);
     return (okx && oky && cx >= 0 && cx < n && cy >= 0 && cy < n) ? r1 * (n * n) + cy * n + cx : -1;
 }
 
@@ -429,11 +471,12 @@ __device__ __forceinline__ bool motion_valid_culled(float minx, float miny, floa
 // v / agentLength: when agentLength is a power of two, v * (1/agentLength) is the
 // same correctly rounded value (both are the exact product scaled by 2^-k), so the
 // host passes invAgentLength != 0 and the per-step division disappears.
-// Predicated instead of the reference's per-lane break: every live lane computes
-// the step; a lane that fails the bounds test keeps its new (x, y) and its old
-// (theta, v), a lane that fails the collision test keeps all four (exactly the
-// state at the reference's break), and later steps leave a dead lane unchanged.
-// The wave leaves the loop once no lane is alive.
+// Exec-masked instead of the reference's per-lane break: a dead lane skips the
+// step body (the wave keeps iterating while any lane is alive); a lane that fails
+// the bounds test keeps its new (x, y) and its old (theta, v), a lane that fails the
+// collision test keeps all four -- exactly the state at the reference's break.
+// Loop-invariant divisions by numDisc / agentLength use div_by when the host
+// verified the reciprocal (bit-exact; tools/check_fast_division.c).
 template <int OBS>
 __device__ __forceinline__ bool propagate_car(float4 p, Xorwow& rs, const KgmtDev& d, const float4* obs,
                                               ChildOut& out) {
@@ -441,7 +484,7 @@ __device__ __forceinline__ bool propagate_car(float4 p, Xorwow& rs, const KgmtDe
     const float u2 = xorwow_uniform(rs);
     const float steering = (float)__builtin_fma((double)(u2 * 2.0f), 3.141592653589793, -3.141592653589793);
     const float duration = __builtin_fmaf(xorwow_uniform(rs), 1.0f, 0.05f);
-    const float dt = duration / (float)d.numDisc;
+    const float dt = div_or_ieee(duration, (float)d.numDisc, d.rcpNumDisc);
     float x = p.x, y = p.y, theta = p.z, v = p.w;
     const float tan_steering = tanf_d(steering);
     // |v| <= |v0| + |a| t, so the displacement stays below T |v0| + |a| T^2 / 2.
@@ -452,12 +495,22 @@ __device__ __forceinline__ bool propagate_car(float4 p, Xorwow& rs, const KgmtDe
     }
     bool alive = true;
     for (int i = 0; i < d.numDisc; ++i) {
+        if (!alive) continue;
         float st, ct;
         sincos_pred(theta, &st, &ct);
         const float nx = __builtin_fmaf(v * ct, dt, x);
         const float ny = __builtin_fmaf(v * st, dt, y);
-        const bool oob = cull.bounds && ((nx <= 0.0f) | (nx >= d.width) | (ny <= 0.0f) | (ny >= d.height));
-        const float vl = (d.invAgentLength != 0.0f) ? v * d.invAgentLength : v / d.agentLength;
+        // min(nx, ny) <= 0 is (nx <= 0) | (ny <= 0) for finite operands (D15)
+        const bool oob = cull.bounds && ((seg_min(nx, ny) <= 0.0f) | (nx >= d.width) | (ny >= d.height));
+        float vl;
+        if (d.invAgentLength != 0.0f) {
+            vl = v * d.invAgentLength;
+        } else {
+            vl = div_by(v, d.agentLength, d.rcpAgentLength);
+            const bool slow = (d.rcpAgentLength == 0.0f) | !(__builtin_fabsf(v) >= 0x1p-100f) |
+                              !(__builtin_fabsf(v) <= 0x1p100f);
+            if (__ballot(slow) != 0ull && slow) vl = v / d.agentLength;
+        }
         const float nth = __builtin_fmaf(vl * tan_steering, dt, theta);
         const float nv = __builtin_fmaf(a, dt, v);
         // (x > nx ? nx : x) etc. as one v_min / v_max.  They differ from the ternaries
@@ -468,16 +521,16 @@ __device__ __forceinline__ bool propagate_car(float4 p, Xorwow& rs, const KgmtDe
         bool freeSeg;
         if (OBS >= kObsReg) freeSeg = motion_valid_culled<OBS>(minx, miny, maxx, maxy, obs, cull.boxes);
         else if (OBS == kObsGrid)   // only lanes whose result counts walk their cells
-            freeSeg = !(alive & !oob) || grid_motion_valid(minx, miny, maxx, maxy, d.gridG, d.gridInvW, d.gridInvH,
-                                                           d.gridStart, d.gridBoxes);
+            freeSeg = oob || grid_motion_valid(minx, miny, maxx, maxy, d.gridG, d.gridInvW, d.gridInvH,
+                                               d.gridStart, d.gridBoxes);
         else freeSeg = motion_valid<OBS>(minx, miny, maxx, maxy, obs, d.nObs);
-        const bool adv = alive & !oob;
-        x = alive ? nx : x;
-        y = alive ? ny : y;
-        theta = adv ? nth : theta;
-        v = adv ? nv : v;
-        alive = adv & freeSeg;
-        if (__ballot(alive) == 0ull) break;
+        x = nx;
+        y = ny;
+        if (!oob) {
+            theta = nth;
+            v = nv;
+        }
+        alive = !oob & freeSeg;
     }
     out.state = make_float4(x, y, theta, v);
     out.a = a;
@@ -493,28 +546,28 @@ __device__ __forceinline__ bool propagate_point(float4 p, Xorwow& rs, const Kgmt
     const float vx = __builtin_fmaf(xorwow_uniform(rs), 2.0f, -1.0f);
     const float vy = __builtin_fmaf(xorwow_uniform(rs), 2.0f, -1.0f);
     const float duration = __builtin_fmaf(xorwow_uniform(rs), 1.0f, 0.05f);
-    const float dt = duration / (float)d.numDisc;
+    const float dt = div_or_ieee(duration, (float)d.numDisc, d.rcpNumDisc);
     float x = p.x, y = p.y;
     WaveCull cull{~0u, true};
     if (OBS >= kObsReg)
         cull = wave_cull<OBS>(p.x, p.y, duration * __builtin_fabsf(vx), duration * __builtin_fabsf(vy), obs, d);
     bool alive = true;
     for (int i = 0; i < d.numDisc; ++i) {
+        if (!alive) continue;
         const float nx = __builtin_fmaf(vx, dt, x);
         const float ny = __builtin_fmaf(vy, dt, y);
-        const bool oob = cull.bounds && ((nx <= 0.0f) | (nx >= d.width) | (ny <= 0.0f) | (ny >= d.height));
+        const bool oob = cull.bounds && ((seg_min(nx, ny) <= 0.0f) | (nx >= d.width) | (ny >= d.height));
         const float minx = seg_min(x, nx), maxx = seg_max(x, nx);   // see propagate_car
         const float miny = seg_min(y, ny), maxy = seg_max(y, ny);
         bool freeSeg;
         if (OBS >= kObsReg) freeSeg = motion_valid_culled<OBS>(minx, miny, maxx, maxy, obs, cull.boxes);
         else if (OBS == kObsGrid)
-            freeSeg = !(alive & !oob) || grid_motion_valid(minx, miny, maxx, maxy, d.gridG, d.gridInvW, d.gridInvH,
-                                                           d.gridStart, d.gridBoxes);
+            freeSeg = oob || grid_motion_valid(minx, miny, maxx, maxy, d.gridG, d.gridInvW, d.gridInvH,
+                                               d.gridStart, d.gridBoxes);
         else freeSeg = motion_valid<OBS>(minx, miny, maxx, maxy, obs, d.nObs);
-        x = alive ? nx : x;
-        y = alive ? ny : y;
-        alive = alive & !oob & freeSeg;
-        if (__ballot(alive) == 0ull) break;
+        x = nx;
+        y = ny;
+        alive = !oob & freeSeg;
     }
     out.state = make_float4(x, y, 0.0f, 0.0f);
     out.a = vx;

@@ -171,7 +171,7 @@ __global__ __launch_bounds__(kBlock) void k_expand(KgmtDev d, int t) {
     const float4 p = d.treeState[parent];
 
     if (tid < d.nR1) sScore[tid] = scoreReg;
-    for (int i = tid; i < d.nR1; i += kBlock) sR1P[i] = 0;
+    sR1P[tid] = 0;   // nR1 == kBlock
 #pragma unroll
     for (int j = 0; j < kMaxR2Words / kBlock; ++j) {
         if (tid + j * kBlock < nW) {
@@ -194,8 +194,8 @@ __global__ __launch_bounds__(kBlock) void k_expand(KgmtDev d, int t) {
         const bool valid = (AGENT == 0) ? propagate_car<OBS>(p, rs, d, obs, out)
                                         : propagate_point<OBS>(p, rs, d, obs, out);
         SBMP_STAMP(2);
-        const int r1 = getR1(out.state.x, out.state.y, d.R1Size, kN);   // N = 16 (KGMT.cu:8)
-        const int r2 = getR2(out.state.x, out.state.y, r1, d.R1Size, kN, d.R2Size, d.n);
+        const int r1 = getR1_k(out.state.x, out.state.y, d.R1Size, d.rcpR1Size, kN);   // N = 16 (KGMT.cu:8)
+        const int r2 = getR2_k(out.state.x, out.state.y, r1, d.R1Size, kN, d.R2Size, d.rcpR2Size, d.n);
         if (valid) {
             const float u = xorwow_uniform(rs);   // KGMT.cu:395
             if (r2 >= 0) {                        // r2 >= 0 implies r1 >= 0
@@ -232,10 +232,8 @@ __global__ __launch_bounds__(kBlock) void k_expand(KgmtDev d, int t) {
     if (tid == 0) d.blockCountOut[gblock] = sWaveCnt[0] + sWaveCnt[1] + sWaveCnt[2] + sWaveCnt[3];
     {   // one 64-bit atomic per touched cell, into this workgroup's replica
         unsigned long long* const rep = d.deltaOut + (size_t)(blockIdx.x % kDeltaReps) * d.nR1;
-        for (int i = tid; i < d.nR1; i += kBlock) {
-            const int v = sR1P[i];
-            if (v) atomicAdd(&rep[i], (unsigned long long)(v & 0xffff) | ((unsigned long long)(v >> 16) << 32));
-        }
+        const int v = sR1P[tid];   // nR1 == kBlock
+        if (v) atomicAdd(&rep[tid], (unsigned long long)(v & 0xffff) | ((unsigned long long)(v >> 16) << 32));
     }
     for (int i = tid; i < nW; i += kBlock) {   // R2New as one byte per cell (sums merge ranks)
         uint32_t w = sNew[i];
@@ -808,7 +806,7 @@ __device__ __forceinline__ void step_scan(const KgmtDev& d, int4 pk, int* sPfx, 
     if (lane == kWave - 1) sRed[0][wave] = incl;
     __syncthreads();
     int base = incl - run;
-    for (int w = 0; w < wave; ++w) base += sRed[0][w];
+    base += (wave > 0 ? sRed[0][0] : 0) + (wave > 1 ? sRed[0][1] : 0) + (wave > 2 ? sRed[0][2] : 0);
     *A = sRed[0][0] + sRed[0][1] + sRed[0][2] + sRed[0][3];
     // Prefixes grow with g and a goal child's in-block index is below its block's
     // count, so the lowest g holding a goal child has the lowest global index.
@@ -1057,6 +1055,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) voi
     __shared__ int sWaveCnt[kBlock / kWave];
     __shared__ int sRed[2][kBlock / kWave];
     __shared__ float sPart[8];
+    __shared__ int sStale;
     __shared__ int sCovInc[kMaxR1];
 
     constexpr bool kLdsObs = (OBS == kObsLds || OBS == kObsLds4);
@@ -1094,7 +1093,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) voi
     const uint2 rb = d.rngB[slot];
     const unsigned long long oldWord = (lane == 0) ? d.gnewOut[slot >> 6] : 0ull;
     const float4 obsReg = (kLdsObs && tid < d.nObs) ? d.obstacles[tid] : make_float4(0.f, 0.f, 0.f, 0.f);
-    for (int i = tid; i < d.nR1; i += kBlock) sR1P[i] = 0;
+    sR1P[tid] = 0;   // nR1 == kBlock
+    if (tid == 0) sStale = 0;
     int A, jGoal;
     step_scan(d, pk, sPfx, sRed, &A, &jGoal);
     SBMP_STAMP(1);
@@ -1226,7 +1226,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) voi
                 }
             }
         }
-        if (!__syncthreads_and(ok)) {
+        if (__ballot(!ok) != 0ull && lane == 0) sStale = 1;   // one barrier, not __syncthreads_and's three
+        __syncthreads();
+        if (sStale) {
             const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
             bool late = false;
             for (;;) {
@@ -1258,8 +1260,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) voi
     float4 cs = make_float4(0.f, 0.f, 0.f, 0.f), cc = cs;   // this slot's child (state, ctrl)
     float cost = 0.0f;
     if (act) {
-        const int q1 = getR1(out.state.x, out.state.y, d.R1Size, kN);   // N = 16 (KGMT.cu:8)
-        const int q2 = getR2(out.state.x, out.state.y, q1, d.R1Size, kN, d.R2Size, d.n);
+        const int q1 = getR1_k(out.state.x, out.state.y, d.R1Size, d.rcpR1Size, kN);   // N = 16 (KGMT.cu:8)
+        const int q2 = getR2_k(out.state.x, out.state.y, q1, d.R1Size, kN, d.R2Size, d.rcpR2Size, d.n);
         if (valid) {
             const float u = xorwow_uniform(rs);   // KGMT.cu:395
             if (q2 >= 0) {
@@ -1290,10 +1292,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) voi
         (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)word, 0);
     const unsigned long long wordAll = word0 | mask;   // GNew |= accept (stale bits survive)
     const bool flagged = (wordAll >> lane) & 1ull;
-    if (flagged && !act) {   // a stale flag on a slot past S: the child last written there
-        cs = d.uState[slot];
-        cc = d.uCtrl[slot];
-        cost = d.treeCtrl[__float_as_int(cc.w)].w + cc.z;
+    if (__ballot(flagged && !act) != 0ull) {   // rare; keeps the wait below off the common path
+        if (flagged && !act) {   // a stale flag on a slot past S: the child last written there
+            cs = d.uState[slot];
+            cc = d.uCtrl[slot];
+            cost = d.treeCtrl[__float_as_int(cc.w)].w + cc.z;
+        }
     }
     bool inGoal = false;
     if (flagged) {
@@ -1307,7 +1311,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) voi
     __syncthreads();
     SBMP_STAMP(5);
     int idx = 0;
-    for (int i = 0; i < wave; ++i) idx += sWaveCnt[i];
+    idx += (wave > 0 ? sWaveCnt[0] : 0) + (wave > 1 ? sWaveCnt[1] : 0) + (wave > 2 ? sWaveCnt[2] : 0);
     const int cntB = sWaveCnt[0] + sWaveCnt[1] + sWaveCnt[2] + sWaveCnt[3];
     idx += __popcll(wordAll & ((1ull << lane) - 1ull));
     if (flagged) {
@@ -1322,15 +1326,17 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) voi
     {   // one 64-bit atomic per touched cell, into this workgroup's replica
         unsigned long long* const rep =
             d.stepDelta + (size_t)(t % 3) * kDeltaReps * d.nR1 + (size_t)(b % kDeltaReps) * d.nR1;
-        for (int i = tid; i < d.nR1; i += kBlock) {
-            const int v = sR1P[i];
-            if (v) atomicAdd(&rep[i], (unsigned long long)(v & 0xffff) | ((unsigned long long)(v >> 16) << 32));
-        }
+        const int v = sR1P[tid];   // nR1 == kBlock
+        if (v) atomicAdd(&rep[tid], (unsigned long long)(v & 0xffff) | ((unsigned long long)(v >> 16) << 32));
     }
     uint32_t* const newCur = d.stepR2New + (size_t)(t % 3) * nW;
-    for (int i = tid; i < nW; i += kBlock) {
-        const uint32_t w = sNew[i];
-        if (w) atomicOr(&newCur[i], w);
+#pragma unroll
+    for (int j = 0; j < kMaxR2Words / kBlock; ++j) {
+        const int i = tid + j * kBlock;
+        if (j * kBlock < nW && i < nW) {
+            const uint32_t w = sNew[i];
+            if (w) atomicOr(&newCur[i], w);
+        }
     }
     __syncthreads();
     if (tid == 0) {

@@ -14,7 +14,9 @@
 #include <cstring>
 #include <fstream>
 #include <iomanip>
+#include <mutex>
 #include <string>
+#include <unordered_map>
 #include <sys/stat.h>
 
 #include "kgmt_launch.h"
@@ -37,6 +39,45 @@ T* KgmtPlanner::alloc(size_t n) {
                     "hipMalloc(" + std::to_string(bytes) + "): " + hipGetErrorString(e));
     allocs_.push_back(p);
     return static_cast<T*>(p);
+}
+
+// RN(1/b) when the kernels' div_by (q0 = a y, r = fma(-q0, b, a), q = fma(r, y, q0))
+// returns RN(a / b) bit for bit for every float a with |a| in [2^-100, 2^100]; else 0,
+// and the kernels divide.  Quotient and residual scale exactly with a's exponent
+// there (b is limited to [2^-20, 2^20], so both stay normal), so checking the 2^23
+// mantissas of one binade covers the range (tools/check_fast_division.c checks all
+// 2^32 inputs for the bench's divisors).  Cached per divisor: ~20 ms each.
+static float markstein_rcp(float b) {
+    static std::mutex mu;
+    static std::unordered_map<uint32_t, float> cache;
+    uint32_t key;
+    std::memcpy(&key, &b, 4);
+    {
+        std::lock_guard<std::mutex> g(mu);
+        auto it = cache.find(key);
+        if (it != cache.end()) return it->second;
+    }
+    float y = 0.0f;
+    if (std::isfinite(b) && std::fabs(b) >= 0x1p-20f && std::fabs(b) <= 0x1p20f) {
+        const volatile float vb = b;
+        y = 1.0f / vb;
+        for (uint32_t m = 0; m < (1u << 23); ++m) {
+            float a;
+            const uint32_t bits = 0x3f800000u | m;   // [1, 2)
+            std::memcpy(&a, &bits, 4);
+            const volatile float ref = a / vb;
+            const volatile float q0 = a * y;
+            const float r = std::fma(-q0, b, a);
+            const float q = std::fma(r, y, (float)q0);
+            if (q != ref) {
+                y = 0.0f;
+                break;
+            }
+        }
+    }
+    std::lock_guard<std::mutex> g(mu);
+    cache[key] = y;
+    return y;
 }
 
 static int round_up(long long x, long long m) { return (int)(((x + m - 1) / m) * m); }
@@ -105,6 +146,10 @@ KgmtPlanner::KgmtPlanner(const sbmp_kgmt_params& p, int nranks, int rank, Exchan
     d.goalThreshold = p.goalThreshold;
     d.R1Size = p.width / (float)p.N;          // KGMT.cu:13
     d.R2Size = p.width / (float)(p.n * p.N);  // KGMT.cu:14
+    d.rcpR1Size = markstein_rcp(d.R1Size);
+    d.rcpR2Size = markstein_rcp(d.R2Size);
+    d.rcpNumDisc = markstein_rcp((float)p.numDisc);
+    d.rcpAgentLength = markstein_rcp(p.agentLength);
 
     d.treeState = alloc<float4>(M);
     d.treeCtrl = alloc<float4>(M);
