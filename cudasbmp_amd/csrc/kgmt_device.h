@@ -477,9 +477,16 @@ __device__ __forceinline__ bool motion_valid_culled(float minx, float miny, floa
 // collision test keeps all four -- exactly the state at the reference's break.
 // Loop-invariant divisions by numDisc / agentLength use div_by when the host
 // verified the reciprocal (bit-exact; tools/check_fast_division.c).
-template <int OBS>
+struct NoMidHook {
+    __device__ void operator()() const {}
+};
+
+// midHook() runs once, at Euler step numDisc / 2, on every lane that entered (k_step
+// issues the planner-publication loads there: late enough to see them, early enough
+// that they have landed when propagation ends).
+template <int OBS, typename MidHook = NoMidHook>
 __device__ __forceinline__ bool propagate_car(float4 p, Xorwow& rs, const KgmtDev& d, const float4* obs,
-                                              ChildOut& out) {
+                                              ChildOut& out, MidHook midHook = MidHook()) {
     const float a = __builtin_fmaf(xorwow_uniform(rs), 10.0f, -5.0f);
     const float u2 = xorwow_uniform(rs);
     const float steering = (float)__builtin_fma((double)(u2 * 2.0f), 3.141592653589793, -3.141592653589793);
@@ -494,7 +501,9 @@ __device__ __forceinline__ bool propagate_car(float4 p, Xorwow& rs, const KgmtDe
         cull = wave_cull<OBS>(p.x, p.y, r, r, obs, d);
     }
     bool alive = true;
+    const int midStep = d.numDisc >> 1;
     for (int i = 0; i < d.numDisc; ++i) {
+        if (i == midStep) midHook();   // uniform
         if (!alive) continue;
         float st, ct;
         sincos_pred(theta, &st, &ct);
@@ -540,9 +549,9 @@ __device__ __forceinline__ bool propagate_car(float4 p, Xorwow& rs, const KgmtDe
 }
 
 // Holonomic R2 point (build extension), predicated like propagate_car.
-template <int OBS>
+template <int OBS, typename MidHook = NoMidHook>
 __device__ __forceinline__ bool propagate_point(float4 p, Xorwow& rs, const KgmtDev& d, const float4* obs,
-                                                ChildOut& out) {
+                                                ChildOut& out, MidHook midHook = MidHook()) {
     const float vx = __builtin_fmaf(xorwow_uniform(rs), 2.0f, -1.0f);
     const float vy = __builtin_fmaf(xorwow_uniform(rs), 2.0f, -1.0f);
     const float duration = __builtin_fmaf(xorwow_uniform(rs), 1.0f, 0.05f);
@@ -552,7 +561,9 @@ __device__ __forceinline__ bool propagate_point(float4 p, Xorwow& rs, const Kgmt
     if (OBS >= kObsReg)
         cull = wave_cull<OBS>(p.x, p.y, duration * __builtin_fabsf(vx), duration * __builtin_fabsf(vy), obs, d);
     bool alive = true;
+    const int midStep = d.numDisc >> 1;
     for (int i = 0; i < d.numDisc; ++i) {
+        if (i == midStep) midHook();   // uniform
         if (!alive) continue;
         const float nx = __builtin_fmaf(vx, dt, x);
         const float ny = __builtin_fmaf(vy, dt, y);

@@ -1177,9 +1177,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) voi
             srcCost = reinterpret_cast<const float*>(src + 2);
         }
     }
-    // Parent, obstacles and the planner's published scores and snapshot of t (checked
-    // after propagation) are issued back to back and waited for together.  The
-    // prefetch addresses are clamped instead of predicated: a load under a divergent
+    // Parent, obstacles (and, for the global-list and grid variants, the planner's
+    // published scores and snapshot of t, checked after propagation) are issued back to
+    // back and waited for together.  The prefetch addresses are clamped instead of predicated: a load under a divergent
     // branch makes the wait ahead of propagation a full vmcnt(0).
     const float4 p = *src;
     const float parentCost = *srcCost;
@@ -1188,13 +1188,22 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) voi
     for (int i = 0; i < kRegObs; ++i) ro[i] = d.obstacles[i];
     const bool pre = nW <= kStepPrefetch * kBlock;
     unsigned long long pubS = 0ull, pubW[kStepPrefetch];
-    if (pre) {
-        pubS = __hip_atomic_load(pubCur + min(tid, d.nR1 - 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    auto loadPub = [&]() {
+        if (pre) {
+            pubS = __hip_atomic_load(pubCur + min(tid, d.nR1 - 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #pragma unroll
-        for (int j = 0; j < kStepPrefetch; ++j)
-            pubW[j] = __hip_atomic_load(pubCur + d.nR1 + min(tid + j * kBlock, nW - 1), __ATOMIC_RELAXED,
-                                        __HIP_MEMORY_SCOPE_AGENT);
-    }
+            for (int j = 0; j < kStepPrefetch; ++j)
+                pubW[j] = __hip_atomic_load(pubCur + d.nR1 + min(tid + j * kBlock, nW - 1), __ATOMIC_RELAXED,
+                                            __HIP_MEMORY_SCOPE_AGENT);
+        }
+    };
+    // The planner publishes ~3 us into the launch, about when the waves start
+    // propagating: loaded here, half the workgroups saw stale tags and paid a re-read
+    // round trip after propagation.  Variants without global loads in the Euler loop
+    // issue them at its midpoint instead (a global load there would make the loop's own
+    // waits cover them); lanes past S, which do not propagate, load after it.
+    constexpr bool kMidPub = kRegObs > 0 || kLdsObs;
+    if (!kMidPub) loadPub();
     insert_prev();
     if (kLdsObs) {
         if (tid < d.nObs) sObs[tid] = obsReg;
@@ -1206,7 +1215,14 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) voi
     Xorwow rs{ra.x, ra.y, ra.z, ra.w, rb.x, rb.y};
     ChildOut out;
     bool valid = false;
-    if (act) valid = (AGENT == 0) ? propagate_car<OBS>(p, rs, d, obs, out) : propagate_point<OBS>(p, rs, d, obs, out);
+    if (kMidPub) {
+        if (act)
+            valid = (AGENT == 0) ? propagate_car<OBS>(p, rs, d, obs, out, loadPub)
+                                 : propagate_point<OBS>(p, rs, d, obs, out, loadPub);
+        else loadPub();
+    } else if (act) {
+        valid = (AGENT == 0) ? propagate_car<OBS>(p, rs, d, obs, out) : propagate_point<OBS>(p, rs, d, obs, out);
+    }
     SBMP_STAMP(3);
     {   // tags must read t; re-read (bounded) what the prefetch got too early
         const unsigned want = (unsigned)t;
