@@ -62,7 +62,7 @@ constexpr int kMaxRegObs = 8;
 constexpr int kMaxRanks = 8;         // ranks of one sharded planning problem (one node)
 constexpr int obs_in_registers(int obs) { return obs >= kObsReg ? obs - kObsReg : 0; }
 constexpr int kTimelineStamps = 8;   // s_memrealtime stamps per k_expand wave (diagnostics)
-constexpr int kFoldEvery = 16;       // iterations per R2 key-log fold (k_fold_r2)
+constexpr int kFoldEvery = 32;       // iterations per R2 key-log fold (k_fold_r2; 32: 0.51 us per iteration vs 0.87 at 16)
 constexpr int kFoldKeys = 65280;     // keys per fold workgroup (< 2^16: packed 16-bit LDS counters)
 constexpr int kLogMaxR2 = 32767;     // the 16-bit key (r2 | valid << 15) holds r2 < 32767
 constexpr uint16_t kNoKey = 0xffff;  // child outside the R2 grid (D3)
