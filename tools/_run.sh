@@ -1,4 +1,4 @@
 mkdir -p gpurun_out
-timeout -k 10 300 python3 bench.py > gpurun_out/b_official.json 2> gpurun_out/b_official.err || { echo "bench rc=$?"; tail -5 gpurun_out/b_official.err; exit 1; }
-tail -1 gpurun_out/b_official.json
-bash tools/profile_round.sh gpurun_out/r01
+timeout -k 10 400 python3 -u -m pytest tests -q -m gpu --timeout 120 --timeout-method thread -p no:cacheprovider > gpurun_out/gpu_tests.log 2>&1 || { grep -E "FAILED|Error" gpurun_out/gpu_tests.log | head -20; tail -3 gpurun_out/gpu_tests.log; exit 1; }
+tail -1 gpurun_out/gpu_tests.log
+bash tools/ab.sh 4 300 prev=_ab/prev new=. || exit 1
