@@ -117,6 +117,9 @@ def test_stepwise_bit_exact(d_obs, obstacles, oracle_lib):
     dict(n=11, maxTreeSize=20000),                      # largest key-log grid (121 KB fold histogram)
     dict(numDisc=1),
     dict(numDisc=25, agentLength=2.5),
+    dict(numDisc=7, agentLength=1.3),                   # reciprocal-multiply division (host-verified divisors)
+    dict(n=3, numDisc=13, agentLength=0.7),
+    dict(agentLength=3e-7, numIterations=5),            # L below 2^-20: no reciprocal, IEEE division of v / L
     dict(samplesPerIteration=8192, batchRule="fill", maxTreeSize=300000, numIterations=12, goalThreshold=0.0),
     dict(samplesPerIteration=3000, batchRule="fill", maxTreeSize=40000, numIterations=40),   # fills the tree
     dict(samplesPerIteration=4096, batchRule="fill", agent="point", maxTreeSize=100000, numIterations=10),
