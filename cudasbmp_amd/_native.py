@@ -63,7 +63,7 @@ class KernelStat(ctypes.Structure):
 EXPORTED_SYMBOLS = (
     "sbmp_abi_version", "sbmp_status_string", "sbmp_last_error", "sbmp_kgmt_default_params",
     "sbmp_kgmt_create", "sbmp_kgmt_destroy", "sbmp_kgmt_plan", "sbmp_kgmt_begin", "sbmp_kgmt_step",
-    "sbmp_kgmt_enqueue", "sbmp_kgmt_sync", "sbmp_kgmt_result", "sbmp_kgmt_stream", "sbmp_kgmt_copy_tree",
+    "sbmp_kgmt_enqueue", "sbmp_kgmt_sync", "sbmp_kgmt_fold", "sbmp_kgmt_result", "sbmp_kgmt_stream", "sbmp_kgmt_copy_tree",
     "sbmp_kgmt_copy_unexplored", "sbmp_kgmt_copy_flags", "sbmp_kgmt_copy_regions", "sbmp_kgmt_num_slots",
     "sbmp_kgmt_copy_rng", "sbmp_kgmt_iter_log", "sbmp_kgmt_export_csv", "sbmp_kgmt_kernel_stats",
     "sbmp_kgmt_reset_kernel_stats", "sbmp_kgmt_set_profiling", "sbmp_kgmt_kernel_samples", "sbmp_kgmt_enqueue_delay",
@@ -105,6 +105,7 @@ def lib():
         "sbmp_kgmt_step": [vp, i, P(i)],
         "sbmp_kgmt_enqueue": [vp, i],
         "sbmp_kgmt_sync": [vp],
+        "sbmp_kgmt_fold": [vp],
         "sbmp_kgmt_result": [vp, P(PlanResult)],
         "sbmp_kgmt_stream": [vp, P(vp)],
         "sbmp_kgmt_copy_tree": [vp, vp, vp, vp, i],

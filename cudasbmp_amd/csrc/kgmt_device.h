@@ -73,6 +73,7 @@ constexpr uint16_t kNoKey = 0xffff;  // child outside the R2 grid (D3)
 constexpr int kDeltaReps = 8;
 constexpr int kMaxStepBlocks = 1024;   // k_step: one int4 of block counts per thread (<= 262,144 slots)
 constexpr int kNoGoalIdx = 0x7fffffff;
+constexpr int kFastDivMax = 1 << 24;   // slot counts up to this use the float-estimate division
 constexpr int kStepEntry = 3;       // k_step list entry: state, (a, steer, dur, parent), (cost, -, -, -)
 // k_step: when iteration t-1 accepted at most this many children, the planner
 // workgroup (idle once it has published) writes all of them into the tree, and the
@@ -226,8 +227,8 @@ SBMP_HD int getR2(float x, float y, int r1, float R1Size, int N, float R2Size, i
     if (r1 < 0) return -1;
     const int cyR1 = r1 / N;
     const int cxR1 = r1 % N;
-    const float lx = x - (float)cxR1 * R1Size;
-    const float ly = y - (float)cyR1 * R1Size;
+    const float lx = __builtin_fmaf(-(float)cxR1, R1Size, x);   // nvcc's contraction of KGMT.cu:620 (D10)
+    const float ly = __builtin_fmaf(-(float)cyR1, R1Size, y);
     bool okx, oky;
     const int cx = cell_of(lx / R2Size, &okx);
     const int cy = cell_of(ly / R2Size, &oky);
@@ -265,8 +266,8 @@ __device__ __forceinline__ int getR2_k(float x, float y, int r1, float R1Size, i
     if (r1 < 0) return -1;
     const int cyR1 = r1 / N;
     const int cxR1 = r1 % N;
-    const float lx = x - (float)cxR1 * R1Size;
-    const float ly = y - (float)cyR1 * R1Size;
+    const float lx = __builtin_fmaf(-(float)cxR1, R1Size, x);   // nvcc's contraction of KGMT.cu:620 (D10)
+    const float ly = __builtin_fmaf(-(float)cyR1, R1Size, y);
     bool okx, oky;
     const int cx = cell_of(div_or_ieee(lx, R2Size, rcpR2), &okx);
     const int cy = cell_of(div_or_ieee(ly, R2Size, rcpR2), &oky);

@@ -31,8 +31,10 @@
 namespace sbmp {
 
 // ------------------------------------------------------------------ helpers
-// a / b for 0 <= a < 2^24, 1 <= b: float estimate (relative error < 2^-21, so
-// off by at most 1 for a < 2^24) + exact integer correction of up to 2 steps.
+// a / b for 0 <= a < 2^24 (kFastDivMax), 1 <= b: float estimate (relative error
+// < 2^-21, so off by at most 1 for a < 2^24) + exact integer correction of up to 2
+// steps (tests/test_fast_division.py checks the bound on the host).  Larger slot
+// counts take the exact integer division (slot_div, a uniform branch).
 __device__ __forceinline__ int div_small(int a, int b) {
     int q = (int)((float)a * __builtin_amdgcn_rcpf((float)b));
     int r = a - q * b;
@@ -41,6 +43,12 @@ __device__ __forceinline__ int div_small(int a, int b) {
     if (r >= b) { ++q; r -= b; }
     if (r >= b) { ++q; }
     return q;
+}
+
+// slot = g * k + i -> g.  nSlots is a per-plan constant, so the branch is uniform.
+__device__ __forceinline__ int slot_div(const KgmtDev& d, int slot, int k) {
+    if (k == 32) return slot >> 5;
+    return (d.nSlots <= kFastDivMax) ? div_small(slot, k) : slot / k;
 }
 
 // The 64-B control block of one iteration with ONE scalar load.  The compiler
@@ -166,7 +174,7 @@ __global__ __launch_bounds__(kBlock) void k_expand(KgmtDev d, int t) {
     // load inside a branch makes the compiler wait with vmcnt(0) at the join, i.e.
     // for this load too before the LDS set-up below.
     const bool act = slot < c.S;
-    const int g = !act ? 0 : (c.k == 32) ? (slot >> 5) : div_small(slot, c.k);   // slot = g*k + i
+    const int g = !act ? 0 : slot_div(d, slot, c.k);   // slot = g*k + i
     const int parent = act ? c.gLo + g : 0;
     const float4 p = d.treeState[parent];
 
@@ -1139,7 +1147,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) voi
 
     // ---- expand t
     const bool act = slot < q.S;
-    const int g = !act ? 0 : (q.k == 32) ? (slot >> 5) : div_small(slot, q.k);   // slot = g*k + i
+    const int g = !act ? 0 : slot_div(d, slot, q.k);   // slot = g*k + i
     const int parent = act ? q.gLo + g : 0;
     const float4* src = d.treeState + parent;   // the parent's state, and its cost
     const float* srcCost = &d.treeCtrl[parent].w;

@@ -45,6 +45,7 @@ public:
     virtual void begin(const float* initial, const float* goal, const float* d_obstacles, int nObs, uint64_t seed) = 0;
     virtual void enqueue(int iterations) = 0;
     virtual void sync() = 0;
+    virtual void fold_pending() = 0;   // enqueue k_fold_r2 up to the last enqueued iteration
     virtual bool active() = 0;   // syncs; false once the loop has ended
     virtual void result(sbmp_plan_result* r) = 0;
     void run(int pollEvery);     // enqueue until the loop ends
@@ -92,6 +93,9 @@ public:
     void begin(const float* initial, const float* goal, const float* d_obstacles, int nObs, uint64_t seed) override;
     void enqueue(int iterations) override;
     void sync() override;
+    void fold_pending() override {
+        if (begun_) fold_to(t_next_ - 1);
+    }
     bool active() override;
     void result(sbmp_plan_result* r) override;
 
@@ -191,6 +195,9 @@ public:
     void begin(const float* initial, const float* goal, const float* d_obstacles, int nObs, uint64_t seed) override;
     void enqueue(int iterations) override;
     void sync() override { r0().sync(); }
+    void fold_pending() override {
+        for (KgmtPlanner* k : ranks_) k->fold_pending();
+    }
     bool active() override { return r0().active(); }
     void result(sbmp_plan_result* r) override { r0().result(r); }
 

@@ -209,6 +209,13 @@ sbmp_status sbmp_kgmt_sync(sbmp_kgmt* h) {
     });
 }
 
+sbmp_status sbmp_kgmt_fold(sbmp_kgmt* h) {
+    return guarded([&] {
+        PLANNER(h);
+        P.fold_pending();
+    });
+}
+
 sbmp_status sbmp_kgmt_result(sbmp_kgmt* h, sbmp_plan_result* result) {
     return guarded([&] {
         PLANNER(h);

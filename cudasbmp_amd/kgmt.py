@@ -202,6 +202,10 @@ class KGMT:
     def sync(self) -> None:
         nat.call("sbmp_kgmt_sync", self._h)
 
+    def fold(self) -> None:
+        """Enqueue the R2Valid / R2Invalid fold of every iteration enqueued so far (no wait)."""
+        nat.call("sbmp_kgmt_fold", self._h)
+
     def result(self) -> nat.PlanResult:
         r = nat.PlanResult()
         nat.call("sbmp_kgmt_result", self._h, ctypes.byref(r))

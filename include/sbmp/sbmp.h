@@ -126,6 +126,11 @@ sbmp_status sbmp_kgmt_step(sbmp_kgmt* h, int iterations, int* active);
  * no-ops once the loop has ended).  sbmp_kgmt_sync waits for the stream. */
 sbmp_status sbmp_kgmt_enqueue(sbmp_kgmt* h, int iterations);
 sbmp_status sbmp_kgmt_sync(sbmp_kgmt* h);
+/* Enqueue, without waiting, the fold of R2Valid / R2Invalid (KGMT.cu:405,410) over
+ * every iteration enqueued so far.  The loop folds its per-child key log every 32
+ * iterations; exports fold the rest themselves.  A timed window calls this before
+ * its closing sync so the deferred work of its own iterations is inside it. */
+sbmp_status sbmp_kgmt_fold(sbmp_kgmt* h);
 sbmp_status sbmp_kgmt_result(sbmp_kgmt* h, sbmp_plan_result* result);
 /* The HIP stream (hipStream_t) every kernel of this planner runs on. */
 sbmp_status sbmp_kgmt_stream(sbmp_kgmt* h, void** stream);

@@ -66,8 +66,9 @@ int getR2(float x, float y, int r1, float R1Size, int N, float R2Size, int n) {
     if (r1 == -1) return -1;
     const int cellY_R1 = r1 / N;
     const int cellX_R1 = r1 % N;
-    const float localX = x - (float)cellX_R1 * R1Size;
-    const float localY = y - (float)cellY_R1 * R1Size;
+    // nvcc contracts x - c * R1Size into fma(-c, R1Size, x) (-fmad=true, D10)
+    const float localX = fmaf(-(float)cellX_R1, R1Size, x);
+    const float localY = fmaf(-(float)cellY_R1, R1Size, y);
     bool okx, oky;
     const int cellX_R2 = to_cell(localX / R2Size, &okx);
     const int cellY_R2 = to_cell(localY / R2Size, &oky);
@@ -92,6 +93,43 @@ bool isMotionValid(const float* bbMin, const float* bbMax, const float* obstacle
     return true;
 }
 
+// Large obstacle lists (the c5 field: 10,000 boxes): the same boolean as
+// isMotionValid, as an order-independent OR over structure-of-arrays copies of the
+// boxes in chunks of 64 (branch-free inside a chunk, so the compiler vectorises it;
+// early exit between chunks).  Any overlapping box makes the segment invalid, so the
+// answer does not depend on the order in which boxes are tested.
+struct ObsSoA {
+    std::vector<float> x0, y0, x1, y1;
+    int n = 0;
+    void assign(const float* obstacles, int count) {
+        n = count;
+        x0.resize(count);
+        y0.resize(count);
+        x1.resize(count);
+        y1.resize(count);
+        for (int i = 0; i < count; ++i) {
+            x0[i] = obstacles[4 * i];
+            y0[i] = obstacles[4 * i + 1];
+            x1[i] = obstacles[4 * i + 2];
+            y1[i] = obstacles[4 * i + 3];
+        }
+    }
+};
+constexpr int kSoAMinObs = 64;
+
+bool isMotionValidSoA(const float* bbMin, const float* bbMax, const ObsSoA& o) {
+    const float bx0 = bbMin[0], by0 = bbMin[1], bx1 = bbMax[0], by1 = bbMax[1];
+    for (int i0 = 0; i0 < o.n; i0 += 64) {
+        const int i1 = std::min(o.n, i0 + 64);
+        int hit = 0;
+        for (int i = i0; i < i1; ++i)   // isBroadPhaseValid negated, NaN-exact (!(a <= b))
+            hit |= (int)(!(bx1 <= o.x0[i])) & (int)(!(o.x1[i] <= bx0)) & (int)(!(by1 <= o.y0[i])) &
+                   (int)(!(o.y1[i] <= by0));
+        if (hit) return false;
+    }
+    return true;
+}
+
 void segment_aabb(const float* v_state, const float* w_state, float* bbMin, float* bbMax) {
     // statePropagator.cu:52-60
     for (int d = 0; d < WS_DIM; ++d) {
@@ -110,7 +148,13 @@ struct PropCfg {
     float agentLength, width, height;
     const float* obstacles;
     int obstaclesCount;
+    const ObsSoA* soa;   // non-null for large lists (isMotionValidSoA)
 };
+
+bool motion_valid(const float* bbMin, const float* bbMax, const PropCfg& c) {
+    if (c.soa) return isMotionValidSoA(bbMin, bbMax, *c.soa);
+    return isMotionValid(bbMin, bbMax, c.obstacles, c.obstaclesCount);
+}
 
 // reference statePropagator.cu:5-76 (propagateAndCheck), car / kinematic bicycle.
 // Contraction choices (D10): a = fmaf(u,10,-5); steering in double with one fma (D11);
@@ -140,7 +184,7 @@ bool propagate_car(const float* x0, float* x1, oracle::XorwowState& rs, const Pr
         const float w_state[WS_DIM] = {x, y};
         float bbMin[WS_DIM], bbMax[WS_DIM];
         segment_aabb(v_state, w_state, bbMin, bbMax);
-        motionValid = motionValid && isMotionValid(bbMin, bbMax, c.obstacles, c.obstaclesCount);
+        motionValid = motionValid && motion_valid(bbMin, bbMax, c);
         if (!motionValid) break;
     }
     x1[0] = x;
@@ -173,7 +217,7 @@ bool propagate_point(const float* x0, float* x1, oracle::XorwowState& rs, const 
         const float w_state[WS_DIM] = {x, y};
         float bbMin[WS_DIM], bbMax[WS_DIM];
         segment_aabb(v_state, w_state, bbMin, bbMax);
-        motionValid = motionValid && isMotionValid(bbMin, bbMax, c.obstacles, c.obstaclesCount);
+        motionValid = motionValid && motion_valid(bbMin, bbMax, c);
         if (!motionValid) break;
     }
     x1[0] = x;
@@ -242,6 +286,7 @@ public:
         R2Invalid_.assign(nR2_, 0);
         obstacles_.assign(obstacles, obstacles + (size_t)nObs * 2 * WS_DIM);
         nObs_ = nObs;
+        soa_.assign(obstacles, nObs);
         memcpy(goal_, goal, sizeof(goal_));
         logs_.clear();
         samplesGenerated_ = 0;
@@ -375,7 +420,8 @@ public:
 
         // D2: the accept test reads R1Score / R2Avail as of the iteration start.
         std::vector<LocalOut> out(S);
-        PropCfg pc{p_.numDisc, p_.agentLength, p_.width, p_.height, obstacles_.data(), nObs_};
+        PropCfg pc{p_.numDisc, p_.agentLength, p_.width, p_.height, obstacles_.data(), nObs_,
+                   nObs_ >= kSoAMinObs ? &soa_ : nullptr};
         const bool point = p_.agent == 1;
 #pragma omp parallel for schedule(static) num_threads(threads())
         for (int s = 0; s < S; ++s) {
@@ -515,6 +561,7 @@ public:
     oracle_iter_log cur_{};
     float goal_[SAMPLE_DIM];
     int nObs_ = 0;
+    ObsSoA soa_;
     int itr_ = 0, treeSize_ = 0, goalIdx_ = -1;
     float costToGoal_ = 0.0f;
     bool terminated_ = false;
@@ -664,7 +711,10 @@ void oracle_xorwow_draw(uint32_t state[6], int count, uint32_t* out) {
 // for numDisc steps; out[i] = (x, y, theta, v), valid[i] = motion validity.
 void oracle_replay(const oracle_params* prm, const float* obstacles, int nObs, const float* parents,
                    const float* controls, int n, float* out, uint8_t* valid) {
-    PropCfg pc{prm->numDisc, prm->agentLength, prm->width, prm->height, obstacles, nObs};
+    ObsSoA soa;
+    soa.assign(obstacles, nObs);
+    PropCfg pc{prm->numDisc, prm->agentLength, prm->width, prm->height, obstacles, nObs,
+               nObs >= kSoAMinObs ? &soa : nullptr};
 #pragma omp parallel for schedule(static) num_threads(prm->threads > 0 ? prm->threads : 1)
     for (int i = 0; i < n; ++i) {
         const float* p = &parents[4 * i];
@@ -695,7 +745,7 @@ void oracle_replay(const oracle_params* prm, const float* obstacles, int nObs, c
             const float w_state[WS_DIM] = {x, y};
             float bbMin[WS_DIM], bbMax[WS_DIM];
             segment_aabb(v_state, w_state, bbMin, bbMax);
-            if (!isMotionValid(bbMin, bbMax, pc.obstacles, pc.obstaclesCount)) {
+            if (!motion_valid(bbMin, bbMax, pc)) {
                 ok = false;
                 break;
             }

@@ -65,6 +65,14 @@ def main():
                             "correction": "read = 2 x FETCH_SIZE (gfx950, MI355X_MICROARCH.md HBM)"}
                 if key in ("k_expand", "k_step") and a.samples_per_launch:
                     out[key]["hbm_bytes_per_child"] = (rd + wr) / a.samples_per_launch
+                    # instruction counts for bench.py's valu_frac / salu_frac / wait_frac
+                    if "SQ_INSTS_VALU" in cs and "SQ_WAVES" in cs:
+                        out[key]["valu_insts_per_child"] = cs["SQ_INSTS_VALU"] / a.samples_per_launch
+                        out[key]["salu_insts_per_child"] = cs["SQ_INSTS_SALU"] / a.samples_per_launch
+                        out[key]["valu_insts_per_wave"] = cs["SQ_INSTS_VALU"] / cs["SQ_WAVES"]
+                        out[key]["salu_insts_per_wave"] = cs["SQ_INSTS_SALU"] / cs["SQ_WAVES"]
+                    if "SQ_WAIT_ANY" in cs and "SQ_WAVE_CYCLES" in cs:
+                        out[key]["wait_any_frac"] = cs["SQ_WAIT_ANY"] / cs["SQ_WAVE_CYCLES"]
         with open(a.json, "w") as f:
             json.dump(out, f, indent=1)
         print("wrote", a.json)
