@@ -55,6 +55,16 @@ class IterRecord(ctypes.Structure):
     _fields_ = [(n, ctypes.c_int) for n in ITER_FIELDS]
 
 
+# sbmp_host_collectives (include/sbmp/sbmp.h): buffers are passed as raw addresses.
+ALLREDUCE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t)
+ALLGATHER_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p)
+
+
+class HostCollectives(ctypes.Structure):
+    _fields_ = [("ctx", ctypes.c_void_p), ("allreduce_u64", ALLREDUCE_FN), ("allreduce_i32", ALLREDUCE_FN),
+                ("allgather", ALLGATHER_FN)]
+
+
 class KernelStat(ctypes.Structure):
     _fields_ = [("name", ctypes.c_char * 32), ("launches", ctypes.c_longlong), ("totalMs", ctypes.c_double)]
 
@@ -69,6 +79,7 @@ EXPORTED_SYMBOLS = (
     "sbmp_kgmt_reset_kernel_stats", "sbmp_kgmt_set_profiling", "sbmp_kgmt_kernel_samples", "sbmp_kgmt_enqueue_delay",
     "sbmp_read_obstacles_csv", "sbmp_device_upload_f32", "sbmp_device_free",
     "sbmp_device_count", "sbmp_comm_get_unique_id", "sbmp_kgmt_create_sharded", "sbmp_kgmt_create_local_group",
+    "sbmp_kgmt_create_sharded_host",
     "sbmp_obstacle_grid_query", "sbmp_kgmt_solution_path", "sbmp_random_tree",
 )
 
@@ -98,6 +109,7 @@ def lib():
         "sbmp_kgmt_create": [P(KgmtParams), P(vp)],
         "sbmp_kgmt_create_sharded": [P(KgmtParams), vp, i, i, P(vp)],
         "sbmp_kgmt_create_local_group": [P(KgmtParams), i, P(vp)],
+        "sbmp_kgmt_create_sharded_host": [P(KgmtParams), P(HostCollectives), i, i, P(vp)],
         "sbmp_comm_get_unique_id": [vp],
         "sbmp_kgmt_destroy": [vp],
         "sbmp_kgmt_plan": [vp, vp, vp, vp, i, ctypes.c_uint64, P(PlanResult)],

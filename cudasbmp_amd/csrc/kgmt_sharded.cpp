@@ -84,11 +84,82 @@ private:
     std::vector<void*> mapped_;
 };
 
-void* sharded_create_comm(const uint8_t* id, int nranks, int rank, int device) {
+// HostExchange: the same protocol with the collectives done by host callbacks
+// (sbmp_host_collectives): the stream is synchronised, the buffer copied to pinned
+// host memory, reduced by the callback, copied back.  The synchronisation makes it
+// the fence RcclExchange's stream order is (every rank's k_pack records are written
+// before any rank returns from the all-reduce).  Record buffers are mapped with HIP
+// IPC as with RCCL, the handles exchanged by the allgather callback.
+class HostExchange : public Exchange {
+public:
+    HostExchange(const sbmp_host_collectives& c, int nranks, int rank, int device)
+        : c_(c), nranks_(nranks), rank_(rank), device_(device) {}
+    ~HostExchange() override {
+        for (void* p : mapped_) (void)hipIpcCloseMemHandle(p);
+        if (host_) (void)hipHostFree(host_);
+    }
+
+    void allreduce_u64(const unsigned long long* send, unsigned long long* recv, size_t n, hipStream_t s) override {
+        reduce(send, recv, n * sizeof(uint64_t), s, [&](void* hs, void* hr) {
+            return c_.allreduce_u64(c_.ctx, static_cast<const uint64_t*>(hs), static_cast<uint64_t*>(hr), n);
+        });
+    }
+    void allreduce_i32(const int* send, int* recv, size_t n, hipStream_t s) override {
+        reduce(send, recv, n * sizeof(int32_t), s, [&](void* hs, void* hr) {
+            return c_.allreduce_i32(c_.ctx, static_cast<const int32_t*>(hs), static_cast<int32_t*>(hr), n);
+        });
+    }
+    void share_buffer(void* own, size_t bytes, void* peers[kMaxRanks]) override {
+        (void)bytes;
+        hipIpcMemHandle_t h;
+        SBMP_HIP(hipIpcGetMemHandle(&h, own));
+        std::vector<hipIpcMemHandle_t> all(nranks_);
+        if (c_.allgather(c_.ctx, &h, sizeof(h), all.data()) != 0)
+            throw Error(SBMP_ERR_COMM, "host allgather of the record-buffer handles failed");
+        for (int q = 0; q < nranks_; ++q) {
+            if (q == rank_) {
+                peers[q] = own;
+                continue;
+            }
+            void* p = nullptr;
+            SBMP_HIP(hipIpcOpenMemHandle(&p, all[q], hipIpcMemLazyEnablePeerAccess));
+            mapped_.push_back(p);
+            peers[q] = p;
+        }
+    }
+
+private:
+    template <typename F>
+    void reduce(const void* send, void* recv, size_t bytes, hipStream_t s, F&& call) {
+        SBMP_HIP(hipSetDevice(device_));
+        if (2 * bytes > hostBytes_) {
+            if (host_) SBMP_HIP(hipHostFree(host_));
+            host_ = nullptr;
+            SBMP_HIP(hipHostMalloc(&host_, 2 * bytes));
+            hostBytes_ = 2 * bytes;
+        }
+        char* hs = static_cast<char*>(host_);
+        char* hr = hs + bytes;
+        SBMP_HIP(hipMemcpyAsync(hs, send, bytes, hipMemcpyDeviceToHost, s));
+        SBMP_HIP(hipStreamSynchronize(s));
+        if (call(hs, hr) != 0) throw Error(SBMP_ERR_COMM, "host all-reduce callback failed");
+        SBMP_HIP(hipMemcpyAsync(recv, hr, bytes, hipMemcpyHostToDevice, s));
+        SBMP_HIP(hipStreamSynchronize(s));
+    }
+
+    sbmp_host_collectives c_;
+    int nranks_, rank_, device_;
+    void* host_ = nullptr;
+    size_t hostBytes_ = 0;
+    std::vector<void*> mapped_;
+};
+
+Exchange* sharded_create_comm(const uint8_t* id, int nranks, int rank, int device) {
     return new RcclExchange(id, nranks, rank, device);
 }
-void sharded_destroy_comm(void* comm) { delete static_cast<RcclExchange*>(comm); }
-Exchange* sharded_exchange(void* comm) { return static_cast<RcclExchange*>(comm); }
+Exchange* sharded_create_host_comm(const sbmp_host_collectives& c, int nranks, int rank, int device) {
+    return new HostExchange(c, nranks, rank, device);
+}
 
 void comm_get_unique_id(uint8_t* id) {
     ncclUniqueId uid;

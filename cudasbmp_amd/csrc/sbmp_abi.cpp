@@ -17,13 +17,12 @@ using sbmp::Planner;
 
 struct sbmp_kgmt {
     Planner* planner = nullptr;
-    void* comm = nullptr;   // sharded: owned collective context (kgmt_sharded.cpp)
+    sbmp::Exchange* comm = nullptr;   // sharded: owned collectives (kgmt_sharded.cpp)
 };
 
 namespace sbmp {
-void* sharded_create_comm(const uint8_t* id, int nranks, int rank, int device);
-void sharded_destroy_comm(void* comm);
-Exchange* sharded_exchange(void* comm);
+Exchange* sharded_create_comm(const uint8_t* id, int nranks, int rank, int device);
+Exchange* sharded_create_host_comm(const sbmp_host_collectives& c, int nranks, int rank, int device);
 void comm_get_unique_id(uint8_t* id);
 }  // namespace sbmp
 
@@ -117,10 +116,31 @@ sbmp_status sbmp_kgmt_create_sharded(const sbmp_kgmt_params* p, const uint8_t id
         sbmp_kgmt* h = new sbmp_kgmt;
         try {
             h->comm = sbmp::sharded_create_comm(id, nranks, rank, p->device);
-            h->planner = new KgmtPlanner(*p, nranks, rank, sbmp::sharded_exchange(h->comm));
+            h->planner = new KgmtPlanner(*p, nranks, rank, h->comm);
         } catch (...) {
             delete h->planner;
-            if (h->comm) sbmp::sharded_destroy_comm(h->comm);
+            delete h->comm;
+            delete h;
+            throw;
+        }
+        *out = h;
+    });
+}
+
+sbmp_status sbmp_kgmt_create_sharded_host(const sbmp_kgmt_params* p, const sbmp_host_collectives* coll, int nranks,
+                                          int rank, sbmp_kgmt** out) {
+    return guarded([&] {
+        REQUIRE(p && coll && out, "NULL argument");
+        REQUIRE(coll->allreduce_u64 && coll->allreduce_i32 && coll->allgather, "NULL collective callback");
+        REQUIRE(nranks >= 1 && rank >= 0 && rank < nranks, "bad rank/nranks");
+        *out = nullptr;
+        sbmp_kgmt* h = new sbmp_kgmt;
+        try {
+            h->comm = sbmp::sharded_create_host_comm(*coll, nranks, rank, p->device);
+            h->planner = new KgmtPlanner(*p, nranks, rank, h->comm);
+        } catch (...) {
+            delete h->planner;
+            delete h->comm;
             delete h;
             throw;
         }
@@ -155,7 +175,7 @@ sbmp_status sbmp_kgmt_destroy(sbmp_kgmt* h) {
     return guarded([&] {
         if (!h) return;
         delete h->planner;
-        if (h->comm) sbmp::sharded_destroy_comm(h->comm);
+        delete h->comm;
         delete h;
     });
 }

@@ -116,7 +116,7 @@ class KGMT:
     def __init__(self, width: float, height: float, N: int, n: int, numIterations: int, maxTreeSize: int,
                  numDisc: int, agentLength: float, goalThreshold: float, *, samplesPerIteration: int = 0,
                  agent: str = "car", fixGNewClear: bool = False, device: int = 0, profileKernels: bool = False,
-                 batchRule: str = "reference", _sharded=None, _local_group: int = 0):
+                 batchRule: str = "reference", _sharded=None, _local_group: int = 0, _host_sharded=None):
         p = nat.KgmtParams()
         nat.call("sbmp_kgmt_default_params", ctypes.byref(p))
         p.width, p.height, p.N, p.n = width, height, N, n
@@ -130,8 +130,14 @@ class KGMT:
         p.batchRule = BATCH_RULES[batchRule]
         self._params = p
         h = ctypes.c_void_p()
+        self._coll = None
         if _local_group:   # sharded data flow with virtual ranks on one device (tests)
             nat.call("sbmp_kgmt_create_local_group", ctypes.byref(p), int(_local_group), ctypes.byref(h))
+        elif _host_sharded is not None:   # sharded, collectives by host callbacks (cudasbmp_amd.host_comm)
+            coll, nranks, rank = _host_sharded
+            self._coll = coll   # the callbacks must outlive the planner
+            nat.call("sbmp_kgmt_create_sharded_host", ctypes.byref(p), ctypes.byref(coll.struct), nranks, rank,
+                     ctypes.byref(h))
         elif _sharded is None:
             nat.call("sbmp_kgmt_create", ctypes.byref(p), ctypes.byref(h))
         else:

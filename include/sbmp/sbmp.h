@@ -223,6 +223,25 @@ sbmp_status sbmp_kgmt_create_sharded(const sbmp_kgmt_params* p, const uint8_t id
  * (exports merge the ranks).  nranks = 1 gives a plain planner. */
 sbmp_status sbmp_kgmt_create_local_group(const sbmp_kgmt_params* p, int nranks, sbmp_kgmt** out);
 
+/* Host collectives for ranks that do not share an RCCL communicator (several
+ * processes on one GPU, or a host program that already runs MPI / gloo).  Each
+ * callback is collective over the nranks ranks and blocking, on host buffers, and
+ * returns 0 on success.  allreduce_*: recv[i] = sum over ranks of send[i];
+ * allgather: recv[q * bytes ..] = rank q's `bytes` bytes of send. */
+typedef struct sbmp_host_collectives {
+    void* ctx;
+    int (*allreduce_u64)(void* ctx, const uint64_t* send, uint64_t* recv, size_t count);
+    int (*allreduce_i32)(void* ctx, const int32_t* send, int32_t* recv, size_t count);
+    int (*allgather)(void* ctx, const void* send, size_t bytes, void* recv);
+} sbmp_host_collectives;
+/* The sharded planner of sbmp_kgmt_create_sharded (same kernels, k_pack records
+ * read over HIP IPC) with its per-iteration all-reduce and the record-buffer
+ * handle exchange done by `coll` on the host: the stream is synchronised, the
+ * fused buffer copied out, reduced, copied back.  *coll is copied; its callbacks
+ * must stay valid until sbmp_kgmt_destroy. */
+sbmp_status sbmp_kgmt_create_sharded_host(const sbmp_kgmt_params* p, const sbmp_host_collectives* coll, int nranks,
+                                          int rank, sbmp_kgmt** out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,106 @@
+"""The cross-process sharded HIP path with two real processes on one GPU.
+
+Each process is one rank of sbmp_kgmt_create_sharded_host: the real k_expand /
+k_pack / k_finish kernels, record buffers written with system-scope stores and
+read by the peer over HIP IPC (hipIpcGetMemHandle / hipIpcOpenMemHandle, handles
+exchanged by an allgather), and the fused exchange buffer all-reduced every
+iteration.  Only RCCL is replaced: RCCL cannot put two ranks on one device, so the
+all-reduce runs over torch.distributed gloo through the host-collectives seam
+(cudasbmp_amd/host_comm.py).  The ranks' merged state must equal the CPU oracle's
+single-rank run bit for bit.
+"""
+import multiprocessing as mp
+import os
+import socket
+
+import numpy as np
+import pytest
+
+from conftest import DEMO, DEMO_GOAL, DEMO_INITIAL, ROOT, bits
+from test_gpu_parity import _oracle
+
+pytestmark = pytest.mark.gpu
+WORLD = 2
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _rank_main(rank, port, kw, seed, out_dir):
+    import sys
+    sys.path.insert(0, ROOT)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=WORLD)
+    from cudasbmp_amd import DeviceBuffer, KGMT
+    from cudasbmp_amd.host_comm import TorchCollectives
+    obs = np.loadtxt(os.path.join(ROOT, "configurations", "obstacles", "obstacles.csv"), delimiter=",",
+                     dtype=np.float32).reshape(-1, 4)
+    cfg = dict(DEMO)
+    extra = {k: kw[k] for k in ("samplesPerIteration", "batchRule", "fixGNewClear") if k in kw}
+    cfg.update({k: v for k, v in kw.items() if k not in extra})
+    g = KGMT(**cfg, **extra, _host_sharded=(TorchCollectives(dist), WORLD, rank))
+    r = g.plan(DEMO_INITIAL, DEMO_GOAL, DeviceBuffer(obs), len(obs), seed=seed)
+    s, p, c = g.tree()
+    G, GN = g.flags()          # GNew words live with their owner: merged by the all-reduce
+    reg = g.regions()          # R2Valid / R2Invalid: each rank folded its own children
+    u, up = g.unexplored()     # slots of other ranks read as 0 / -1
+    rng = g.rng()
+    np.savez(os.path.join(out_dir, f"rank{rank}.npz"), s=s, p=p, c=c, G=G, GN=GN, u=u, up=up, rng=rng,
+             log=g.iter_log(), res=np.array([r.iterations, r.treeSize, r.goalIndex]),
+             cost=np.float32(r.costToGoal), **{"reg_" + k: v for k, v in reg.items()})
+    g.close()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("kw,seed", [
+    (dict(), 3),
+    (dict(samplesPerIteration=4096, batchRule="fill", maxTreeSize=200000, numIterations=15, goalThreshold=0.0), 21),
+    (dict(fixGNewClear=True, numIterations=40), 8),
+])
+def test_two_processes_one_gpu_bit_exact(kw, seed, tmp_path, obstacles, oracle_lib):
+    ctx = mp.get_context("spawn")
+    port = _free_port()
+    procs = [ctx.Process(target=_rank_main, args=(r, port, kw, seed, str(tmp_path))) for r in range(WORLD)]
+    for pr in procs:
+        pr.start()
+    for pr in procs:
+        pr.join(timeout=240)
+    for pr in procs:
+        if pr.is_alive():
+            pr.kill()
+            pr.join()
+    assert [pr.exitcode for pr in procs] == [0] * WORLD, f"rank exit codes {[pr.exitcode for pr in procs]}"
+    R = [np.load(os.path.join(tmp_path, f"rank{r}.npz")) for r in range(WORLD)]
+
+    cfg = dict(DEMO)
+    extra = {k: kw[k] for k in ("samplesPerIteration", "batchRule", "fixGNewClear") if k in kw}
+    cfg.update({k: v for k, v in kw.items() if k not in extra})
+    o = _oracle(cfg, extra)
+    o.plan(DEMO_INITIAL, DEMO_GOAL, obstacles, seed)
+    so, po, co = o.tree()
+    Go, GNo = o.flags()
+    uo, upo = o.unexplored()
+    ro = o.regions()
+    info = o.info()
+    n = o.rng().shape[0]
+    owner = (np.arange(n) // 256) % WORLD
+    for r, d in enumerate(R):   # every rank holds the whole tree and the merged exports
+        assert np.array_equal(d["log"], o.iter_logs()), f"rank {r}: iteration logs differ"
+        assert np.array_equal(d["p"], po), f"rank {r}: parents differ"
+        assert np.array_equal(bits(d["s"]), bits(so)), f"rank {r}: tree samples differ"
+        assert np.array_equal(bits(d["c"]), bits(co)), f"rank {r}: costs differ"
+        assert np.array_equal(d["G"], Go) and np.array_equal(d["GN"], GNo), f"rank {r}: G / GNew differ"
+        for k in ro:
+            assert np.array_equal(bits(d["reg_" + k]), bits(ro[k])), f"rank {r}: {k} differs"
+        assert d["res"].tolist() == [info["iterations"], info["treeSize"], info["goalIdx"]]
+        assert bits(np.float32(d["cost"])) == bits(np.float32(info["costToGoal"]))
+        own = owner == r   # slot state lives with its owner only
+        assert np.array_equal(d["rng"][own], o.rng()[own]), f"rank {r}: RNG states differ"
+        assert np.array_equal(d["up"][:n][own], upo[:n][own]) and \
+            np.array_equal(bits(d["u"][:n][own]), bits(uo[:n][own])), f"rank {r}: unexplored slots differ"
+        assert (d["up"][:n][~own] == -1).all()
