@@ -170,23 +170,28 @@ struct KgmtDev {
 
 // 16-B / 8-B stores with sc1: written through to memory during the kernel, so the
 // dependent kernel boundary has fewer dirty L2 lines to write back (MI355X_MICROARCH.md,
-// "boundary": + dirty bytes / 6 TB/s).  A VMEM store of more than 8 B reads its data
-// VGPRs after issue and the hazard recognizer does not see stores inside inline asm:
-// the s_nop keeps the next VALU from overwriting the data first.
+// "boundary": + dirty bytes / 6 TB/s).  Raw buffer stores carry the cache policy as a
+// builtin operand, so the compiler schedules them and pads their hazards itself (an
+// inline-asm global_store needed a hand-placed s_nop for the >8-B store-data hazard).
+// One V# per array (base, no stride, byte bound 2^31 - 1: every per-slot array here is
+// far smaller); `i` is the element index.
 typedef uint32_t sbmp_u32x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t sbmp_u32x2 __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ void store_wt(void* p, sbmp_u32x4 v) {
-    asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" : : "v"(p), "v"(v) : "memory");
+constexpr int kCpolSc1 = 16;            // gfx94x / gfx950 cache policy: SC1 (write through)
+constexpr int kBufferDword3 = 0x00020000;   // raw-buffer V# word 3 for gfx9 (ck.hpp CK_BUFFER_RESOURCE_3RD_DWORD)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t wt_rsrc(const void* base) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, 0x7fffffff, kBufferDword3);
 }
-__device__ __forceinline__ void store_wt(float4* p, float4 v) {
-    store_wt(static_cast<void*>(p), sbmp_u32x4{__float_as_uint(v.x), __float_as_uint(v.y), __float_as_uint(v.z),
-                                               __float_as_uint(v.w)});
+__device__ __forceinline__ void store_wt(float4* base, int i, float4 v) {
+    __builtin_amdgcn_raw_buffer_store_b128(
+        sbmp_u32x4{__float_as_uint(v.x), __float_as_uint(v.y), __float_as_uint(v.z), __float_as_uint(v.w)},
+        wt_rsrc(base), i * 16, 0, kCpolSc1);
 }
-__device__ __forceinline__ void store_wt(uint4* p, uint4 v) {
-    store_wt(static_cast<void*>(p), sbmp_u32x4{v.x, v.y, v.z, v.w});
+__device__ __forceinline__ void store_wt(uint4* base, int i, uint4 v) {
+    __builtin_amdgcn_raw_buffer_store_b128(sbmp_u32x4{v.x, v.y, v.z, v.w}, wt_rsrc(base), i * 16, 0, kCpolSc1);
 }
-__device__ __forceinline__ void store_wt(uint2* p, uint2 v) {
-    asm volatile("global_store_dwordx2 %0, %1, off sc1" : : "v"(p), "v"(sbmp_u32x2{v.x, v.y}) : "memory");
+__device__ __forceinline__ void store_wt(uint2* base, int i, uint2 v) {
+    __builtin_amdgcn_raw_buffer_store_b64(sbmp_u32x2{v.x, v.y}, wt_rsrc(base), i * 8, 0, kCpolSc1);
 }
 
 // Inclusive prefix sum over the 64 lanes of a wave with DPP: shifts by 1, 2, 4, 8

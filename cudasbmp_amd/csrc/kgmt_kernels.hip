@@ -51,27 +51,19 @@ __device__ __forceinline__ int slot_div(const KgmtDev& d, int slot, int k) {
     return (d.nSlots <= kFastDivMax) ? div_small(slot, k) : slot / k;
 }
 
-// The 64-B control block of one iteration with ONE scalar load.  The compiler
-// reads it with vector loads (the launch also stores ctrl[t].executed, so it
-// cannot prove the line unclobbered, and it folds a constant-address-space cast
-// back to global): each then waits with vmcnt(0) behind every older vector load
-// (XORWOW states, snapshot words), which serialised the prologue.  A scalar load
-// waits on lgkmcnt only.  The fields read here are written by the previous launch;
-// this launch writes only .executed, which it never reads.  The "memory" clobber
-// keeps the independent vector loads issued above it.
-// The goal status (written by earlier launches only) comes with it.
+// The 64-B control block of one iteration with ONE scalar load: a read through the
+// constant address space (4), which the compiler lowers to s_load_dwordx16.  A
+// vector load would wait with vmcnt(0) behind every older vector load (XORWOW
+// states, snapshot words), which serialised the prologue; a scalar load waits on
+// lgkmcnt only.  The fields read here are written by the previous launch; this
+// launch writes only .executed, which it never reads.  The goal status (written by
+// earlier launches only) comes with it.
 typedef int sbmp_i32x16 __attribute__((ext_vector_type(16)));
+typedef const __attribute__((address_space(4))) sbmp_i32x16 sbmp_const_i32x16;
+typedef const __attribute__((address_space(4))) int sbmp_const_i32;
 __device__ __forceinline__ IterCtrl load_ctrl(const IterCtrl* p, const PlannerStatus* st, int* goalIdx) {
-    sbmp_i32x16 v;
-    int g;
-    // Early-clobber outputs: the second load must not take its address from registers
-    // the first one is filling (it did: the status address landed inside v, and a
-    // fast return of the control block turned it into a wild pointer).
-    asm volatile("s_load_dwordx16 %0, %2, 0x0\n\ts_load_dword %1, %3, 0x0\n\ts_waitcnt lgkmcnt(0)"
-                 : "=&s"(v), "=&s"(g)
-                 : "s"(p), "s"(st)
-                 : "memory");
-    *goalIdx = g;
+    const sbmp_i32x16 v = *(sbmp_const_i32x16*)p;   // C cast: address-space casts are not reinterpret_casts
+    *goalIdx = *(sbmp_const_i32*)st;
     IterCtrl c;
     c.run = v[0];
     c.executed = v[1];
@@ -213,10 +205,10 @@ __global__ __launch_bounds__(kBlock) void k_expand(KgmtDev d, int t) {
                 if (!r2Avail) atomicOr(&sNew[r2 >> 5], bit);
             }
         }
-        store_wt(d.uState + slot, out.state);   // write-through: fewer dirty lines at the boundary
-        store_wt(d.uCtrl + slot, make_float4(out.a, out.steer, out.dur, __int_as_float(parent)));
-        store_wt(d.rngA + slot, make_uint4(rs.v0, rs.v1, rs.v2, rs.v3));
-        store_wt(d.rngB + slot, make_uint2(rs.v4, rs.d));
+        store_wt(d.uState, slot, out.state);   // write-through: fewer dirty lines at the boundary
+        store_wt(d.uCtrl, slot, make_float4(out.a, out.steer, out.dur, __int_as_float(parent)));
+        store_wt(d.rngA, slot, make_uint4(rs.v0, rs.v1, rs.v2, rs.v3));
+        store_wt(d.rngB, slot, make_uint2(rs.v4, rs.d));
         if (r1 >= 0) atomicAdd(&sR1P[r1], valid ? 1 : 0x10000);
         if (d.r2log) {
             d.r2log[(size_t)(t % kFoldEvery) * d.logSlots + (int)blockIdx.x * kBlock + tid] =
@@ -1298,10 +1290,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) voi
         cs = out.state;
         cc = make_float4(out.a, out.steer, out.dur, __int_as_float(parent));
         cost = parentCost + out.dur;   // getCost (KGMT.cu:631-633), as the insert computes it
-        store_wt(d.uState + slot, cs);   // write-through: fewer dirty lines at the boundary
-        store_wt(d.uCtrl + slot, cc);
-        store_wt(d.rngA + slot, make_uint4(rs.v0, rs.v1, rs.v2, rs.v3));
-        store_wt(d.rngB + slot, make_uint2(rs.v4, rs.d));
+        store_wt(d.uState, slot, cs);   // write-through: fewer dirty lines at the boundary
+        store_wt(d.uCtrl, slot, cc);
+        store_wt(d.rngA, slot, make_uint4(rs.v0, rs.v1, rs.v2, rs.v3));
+        store_wt(d.rngB, slot, make_uint2(rs.v4, rs.d));
         if (q1 >= 0) atomicAdd(&sR1P[q1], valid ? 1 : 0x10000);
         if (d.r2log) {
             d.r2log[(size_t)(t % kFoldEvery) * d.logSlots + b * kBlock + tid] =
