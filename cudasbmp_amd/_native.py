@@ -65,6 +65,23 @@ class HostCollectives(ctypes.Structure):
                 ("allgather", ALLGATHER_FN)]
 
 
+class ExpandBatchArgs(ctypes.Structure):   # sbmp_expand_batch_args
+    _fields_ = [("count", ctypes.c_int), ("parents", ctypes.c_void_p), ("rng", ctypes.c_void_p),
+                ("obstacles", ctypes.c_void_p), ("obstaclesCount", ctypes.c_int), ("agent", ctypes.c_int),
+                ("numDisc", ctypes.c_int), ("agentLength", ctypes.c_float), ("width", ctypes.c_float),
+                ("height", ctypes.c_float), ("N", ctypes.c_int), ("n", ctypes.c_int), ("R1Score", ctypes.c_void_p),
+                ("R2Avail", ctypes.c_void_p), ("children", ctypes.c_void_p), ("valid", ctypes.c_void_p),
+                ("r1", ctypes.c_void_p), ("r2", ctypes.c_void_p), ("accept", ctypes.c_void_p)]
+
+
+class InsertBatchArgs(ctypes.Structure):   # sbmp_insert_batch_args
+    _fields_ = [("slots", ctypes.c_int), ("gnew", ctypes.c_void_p), ("unexplored", ctypes.c_void_p),
+                ("uParent", ctypes.c_void_p), ("samples", ctypes.c_void_p), ("parent", ctypes.c_void_p),
+                ("costs", ctypes.c_void_p), ("treeSize", ctypes.c_int), ("maxTreeSize", ctypes.c_int),
+                ("goalX", ctypes.c_float), ("goalY", ctypes.c_float), ("goalThreshold", ctypes.c_float),
+                ("fixGNewClear", ctypes.c_int), ("inserted", ctypes.c_void_p), ("goalIndex", ctypes.c_void_p)]
+
+
 class KernelStat(ctypes.Structure):
     _fields_ = [("name", ctypes.c_char * 32), ("launches", ctypes.c_longlong), ("totalMs", ctypes.c_double)]
 
@@ -79,7 +96,8 @@ EXPORTED_SYMBOLS = (
     "sbmp_kgmt_reset_kernel_stats", "sbmp_kgmt_set_profiling", "sbmp_kgmt_kernel_samples", "sbmp_kgmt_enqueue_delay",
     "sbmp_read_obstacles_csv", "sbmp_device_upload_f32", "sbmp_device_free",
     "sbmp_device_count", "sbmp_comm_get_unique_id", "sbmp_kgmt_create_sharded", "sbmp_kgmt_create_local_group",
-    "sbmp_kgmt_create_sharded_host",
+    "sbmp_kgmt_create_sharded_host", "sbmp_expand_batch", "sbmp_expand_batch_host", "sbmp_insert_batch",
+    "sbmp_device_alloc", "sbmp_device_copy_to", "sbmp_device_copy_from",
     "sbmp_obstacle_grid_query", "sbmp_kgmt_solution_path", "sbmp_random_tree",
 )
 
@@ -110,6 +128,12 @@ def lib():
         "sbmp_kgmt_create_sharded": [P(KgmtParams), vp, i, i, P(vp)],
         "sbmp_kgmt_create_local_group": [P(KgmtParams), i, P(vp)],
         "sbmp_kgmt_create_sharded_host": [P(KgmtParams), P(HostCollectives), i, i, P(vp)],
+        "sbmp_expand_batch": [P(ExpandBatchArgs), vp],
+        "sbmp_expand_batch_host": [P(ExpandBatchArgs)],
+        "sbmp_insert_batch": [P(InsertBatchArgs), vp],
+        "sbmp_device_alloc": [ctypes.c_size_t, P(vp)],
+        "sbmp_device_copy_to": [vp, vp, ctypes.c_size_t],
+        "sbmp_device_copy_from": [vp, vp, ctypes.c_size_t],
         "sbmp_comm_get_unique_id": [vp],
         "sbmp_kgmt_destroy": [vp],
         "sbmp_kgmt_plan": [vp, vp, vp, vp, i, ctypes.c_uint64, P(PlanResult)],

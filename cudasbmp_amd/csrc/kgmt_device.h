@@ -15,8 +15,11 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "sbmp/collision.h"
+#include "sbmp/grid.h"
 #include "sbmp/obstacle_grid.h"
 #include "sbmp/sbmp_math.h"
+#include "sbmp/xorwow.h"
 
 #if defined(__clang__)
 #pragma clang fp contract(off)
@@ -214,31 +217,7 @@ __device__ __forceinline__ int first_lane_value(bool pick, int v, int fallback) 
 }
 
 // ---------------------------------------------------------------- grid binning
-// reference KGMT.cu:602-609 / 610-629.  Float->int truncates toward zero; an
-// out-of-int-range or NaN quotient maps to -1 (D3).
-SBMP_HD int cell_of(float q, bool* ok) {
-    *ok = (q > -2147483648.0f && q < 2147483648.0f);
-    return *ok ? (int)q : 0;
-}
-
-SBMP_HD int getR1(float x, float y, float R1Size, int N) {
-    bool okx, oky;
-    const int cx = cell_of(x / R1Size, &okx);
-    const int cy = cell_of(y / R1Size, &oky);
-    return (okx && oky && cx >= 0 && cx < N && cy >= 0 && cy < N) ? cy * N + cx : -1;
-}
-
-SBMP_HD int getR2(float x, float y, int r1, float R1Size, int N, float R2Size, int n) {
-    if (r1 < 0) return -1;
-    const int cyR1 = r1 / N;
-    const int cxR1 = r1 % N;
-    const float lx = __builtin_fmaf(-(float)cxR1, R1Size, x);   // nvcc's contraction of KGMT.cu:620 (D10)
-    const float ly = __builtin_fmaf(-(float)cyR1, R1Size, y);
-    bool okx, oky;
-    const int cx = cell_of(lx / R2Size, &okx);
-    const int cy = cell_of(ly / R2Size, &oky);
-    return (okx && oky && cx >= 0 && cx < n && cy >= 0 && cy < n) ? r1 * (n * n) + cy * n + cx : -1;
-}
+// getR1 / getR2 with the reference's signatures: include/sbmp/grid.h.
 
 // a / b for a per-plan constant b, given y = RN(1/b) computed on the host (Markstein):
 // q0 = RN(a y), r = a - q0 b exactly by FMA, RN(q0 + r y) = RN(a / b) while r stays
@@ -280,46 +259,12 @@ __device__ __forceinline__ int getR2_k(float x, float y, int r1, float R1Size, i
 }
 
 // ---------------------------------------------------------------- cuRAND XORWOW
-struct Xorwow {
-    uint32_t v0, v1, v2, v3, v4, d;
-};
-
-SBMP_HD uint32_t xorwow_next(Xorwow& s) {
-    const uint32_t t = s.v0 ^ (s.v0 >> 2);
-    s.v0 = s.v1;
-    s.v1 = s.v2;
-    s.v2 = s.v3;
-    s.v3 = s.v4;
-    s.v4 = (s.v4 ^ (s.v4 << 4)) ^ (t ^ (t << 1));
-    s.d += 362437u;
-    return s.v4 + s.d;
-}
-
-// curand_init(seed, 0, 0): cuRAND's XORWOW seeding (_curand_init_scratch: salts
-// 0xaad26b49 / 0xf7dcefdd, multipliers 1099087573 / 2591861531), no skip-ahead.
-SBMP_HD Xorwow xorwow_seed(uint64_t seed) {
-    const uint32_t s0 = (uint32_t)seed ^ 0xaad26b49u;
-    const uint32_t s1 = (uint32_t)(seed >> 32) ^ 0xf7dcefddu;
-    const uint32_t t0 = 1099087573u * s0;
-    const uint32_t t1 = 2591861531u * s1;
-    Xorwow st;
-    st.d = 6615241u + t1 + t0;
-    st.v0 = 123456789u + t0;
-    st.v1 = 362436069u ^ t0;
-    st.v2 = 521288629u + t1;
-    st.v3 = 88675123u ^ t1;
-    st.v4 = 5783321u + t0;
-    return st;
-}
-
-// curand_uniform: x * 2^-32 + 2^-33 (product exact, one rounding).
-SBMP_HD float xorwow_uniform(Xorwow& s) {
-    return (float)xorwow_next(s) * 2.3283064365386963e-10f + 1.1641532182693481e-10f;
-}
+// Xorwow, xorwow_next / xorwow_seed / xorwow_uniform: include/sbmp/xorwow.h.
 
 // ---------------------------------------------------------------- collision
-// reference collisionCheck.cu:6-28: a segment AABB is free of an obstacle box
-// iff separated on some axis; the motion is valid iff free of every box.
+// reference collisionCheck.cu:6-28 (isBroadPhaseValid / isMotionValid with the
+// reference's signatures: include/sbmp/collision.h): a segment AABB is free of an
+// obstacle box iff separated on some axis; the motion is valid iff free of every box.
 // Register and LDS forms test every box without early exit (no load->compare->
 // branch chain; the result is an order-independent OR, so identical to the
 // reference's early return); the global form keeps the reference's early exit.

@@ -24,6 +24,9 @@ namespace sbmp {
 Exchange* sharded_create_comm(const uint8_t* id, int nranks, int rank, int device);
 Exchange* sharded_create_host_comm(const sbmp_host_collectives& c, int nranks, int rank, int device);
 void comm_get_unique_id(uint8_t* id);
+void expand_batch(const sbmp_expand_batch_args* args, void* stream);   // batch.hip
+void expand_batch_host(const sbmp_expand_batch_args* args);
+void insert_batch(const sbmp_insert_batch_args* args, void* stream);
 }  // namespace sbmp
 
 static thread_local std::string g_last_error;
@@ -162,6 +165,18 @@ sbmp_status sbmp_kgmt_create_local_group(const sbmp_kgmt_params* p, int nranks, 
         }
         *out = h;
     });
+}
+
+sbmp_status sbmp_expand_batch(const sbmp_expand_batch_args* args, void* stream) {
+    return guarded([&] { sbmp::expand_batch(args, stream); });
+}
+
+sbmp_status sbmp_expand_batch_host(const sbmp_expand_batch_args* args) {
+    return guarded([&] { sbmp::expand_batch_host(args); });
+}
+
+sbmp_status sbmp_insert_batch(const sbmp_insert_batch_args* args, void* stream) {
+    return guarded([&] { sbmp::insert_batch(args, stream); });
 }
 
 sbmp_status sbmp_comm_get_unique_id(uint8_t id[SBMP_COMM_ID_BYTES]) {
@@ -457,6 +472,28 @@ sbmp_status sbmp_device_upload_f32(const float* host, size_t count, float** d_ou
 sbmp_status sbmp_device_free(void* d_ptr) {
     return guarded([&] {
         if (d_ptr) SBMP_HIP(hipFree(d_ptr));
+    });
+}
+
+sbmp_status sbmp_device_alloc(size_t bytes, void** d_out) {
+    return guarded([&] {
+        REQUIRE(d_out, "NULL output pointer");
+        *d_out = nullptr;
+        SBMP_HIP(hipMalloc(d_out, bytes > 0 ? bytes : 1));
+    });
+}
+
+sbmp_status sbmp_device_copy_to(void* d_dst, const void* host, size_t bytes) {
+    return guarded([&] {
+        REQUIRE(bytes == 0 || (d_dst && host), "NULL pointer");
+        if (bytes) SBMP_HIP(hipMemcpy(d_dst, host, bytes, hipMemcpyHostToDevice));
+    });
+}
+
+sbmp_status sbmp_device_copy_from(void* host, const void* d_src, size_t bytes) {
+    return guarded([&] {
+        REQUIRE(bytes == 0 || (d_src && host), "NULL pointer");
+        if (bytes) SBMP_HIP(hipMemcpy(host, d_src, bytes, hipMemcpyDeviceToHost));
     });
 }
 

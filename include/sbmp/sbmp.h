@@ -202,9 +202,69 @@ sbmp_status sbmp_random_tree(int device, int kind, const float* root, int rows, 
 sbmp_status sbmp_obstacle_grid_query(const float* obstacles, int nObs, float width, float height, int gridSize,
                                      const float* segments, int nSegments, uint8_t* freeOut, int* gridUsed);
 
+/* ---- Step-level entry points (one stage of the iteration over caller buffers, so each
+ * can be parity-tested alone) ----
+ *
+ * sbmp_expand_batch: propagateG's per-child work (KGMT.cu:386-411): child i expands
+ * the parent state parents[7 i .. 7 i + 3] with the XORWOW state rng[6 i .. 6 i + 5]
+ * (advanced in place) through propagateAndCheck (include/sbmp/propagator.h, the car;
+ * propagatePoint for agent = SBMP_AGENT_POINT), then getR1 / getR2
+ * (include/sbmp/grid.h) and, if R1Score and R2Avail are given, the accept test
+ * (u <= R1Score[r1] || !R2Avail[r2], one more draw for a valid child; KGMT.cu:394-400).
+ * Every pointer is device memory; valid / r1 / r2 / accept may be NULL.
+ * sbmp_expand_batch_host runs the same code on the CPU over host buffers. */
+typedef struct sbmp_expand_batch_args {
+    int count;                       /* children */
+    const float* parents;            /* count x 7 */
+    uint32_t* rng;                   /* count x 6: v0..v4, d */
+    const float* obstacles;          /* obstaclesCount x [xmin, ymin, xmax, ymax] */
+    int obstaclesCount;
+    int agent;                       /* SBMP_AGENT_CAR / SBMP_AGENT_POINT */
+    int numDisc;
+    float agentLength, width, height;
+    int N, n;                        /* region grid: R1Size = width / N, R2Size = width / (N n) */
+    const float* R1Score;            /* N*N, or NULL: no accept test */
+    const int* R2Avail;              /* N*N*n*n 0/1 */
+    float* children;                 /* count x 7 out: [x, y, theta, v, a, steering, duration] */
+    uint8_t* valid;                  /* count out */
+    int* r1;                         /* count out (-1: outside the grid) */
+    int* r2;                         /* count out */
+    uint8_t* accept;                 /* count out */
+} sbmp_expand_batch_args;
+sbmp_status sbmp_expand_batch(const sbmp_expand_batch_args* args, void* stream /* hipStream_t; NULL: default */);
+sbmp_status sbmp_expand_batch_host(const sbmp_expand_batch_args* args);
+
+/* sbmp_insert_batch: exclusive_scan(GNew) + findInd + updateG (KGMT.cu:221-249,
+ * 540-593): the flagged slots, in slot order, become tree rows treeSize + j with
+ * parent uParent[slot] and cost = costs[parent] + duration (getCost, KGMT.cu:631-633);
+ * min(A, 32 floor(M/32)) rows are written (the updateG grid, KGMT.cu:231), none at or
+ * past maxTreeSize (D13); then GNew[0 .. 32 min(A, M/32)) is cleared (D6), all of it
+ * with fixGNewClear.  *inserted = A, *goalIndex = the lowest new row within
+ * goalThreshold of (goalX, goalY) or -1 (D4).  Device buffers; inserted / goalIndex
+ * are device ints. */
+typedef struct sbmp_insert_batch_args {
+    int slots;
+    uint8_t* gnew;                   /* slots: accept flags (cleared as above) */
+    const float* unexplored;         /* slots x 7 */
+    const int* uParent;              /* slots */
+    float* samples;                  /* maxTreeSize x 7 */
+    int* parent;                     /* maxTreeSize */
+    float* costs;                    /* maxTreeSize */
+    int treeSize, maxTreeSize;
+    float goalX, goalY, goalThreshold;
+    int fixGNewClear;
+    int* inserted;                   /* 1 */
+    int* goalIndex;                  /* 1 */
+} sbmp_insert_batch_args;
+sbmp_status sbmp_insert_batch(const sbmp_insert_batch_args* args, void* stream);
+
 /* Device memory helpers replacing demos/main.cu:60-61,64 (cudaMalloc/cudaMemcpy/cudaFree). */
 sbmp_status sbmp_device_upload_f32(const float* host, size_t count, float** d_out);
 sbmp_status sbmp_device_free(void* d_ptr);
+/* Raw device buffers for the step-level entry points: allocate, copy in, copy out. */
+sbmp_status sbmp_device_alloc(size_t bytes, void** d_out);
+sbmp_status sbmp_device_copy_to(void* d_dst, const void* host, size_t bytes);
+sbmp_status sbmp_device_copy_from(void* host, const void* d_src, size_t bytes);
 sbmp_status sbmp_device_count(int* count);
 
 /* ---- Multi-GPU: one planning problem sharded over ranks (one process per GPU) ----

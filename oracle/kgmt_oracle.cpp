@@ -803,6 +803,44 @@ void oracle_random_tree(int kind, const float* root, int rows, int blocks, int t
     }
 }
 
+// One batch of propagateG's per-child work (KGMT.cu:386-411, statePropagator.cu:5-76):
+// child i expands parents[7 i ..] with RNG state rng[6 i ..] (advanced in place), then
+// getR1 / getR2 and, when scores are given, the accept test against R1Score /
+// R2Avail (KGMT.cu:394-400; D3: a valid child outside the grid is rejected).  The
+// checker of sbmp_expand_batch.
+void oracle_expand_batch(const oracle_params* prm, const float* obstacles, int nObs, const float* parents,
+                         uint32_t* rng, int n, const float* R1Score, const int* R2Avail, float* children,
+                         uint8_t* valid, int* r1, int* r2, uint8_t* accept) {
+    ObsSoA soa;
+    soa.assign(obstacles, nObs);
+    PropCfg pc{prm->numDisc, prm->agentLength, prm->width, prm->height, obstacles, nObs,
+               nObs >= kSoAMinObs ? &soa : nullptr};
+    const float R1Size = prm->width / (float)prm->N;
+    const float R2Size = prm->width / (float)(prm->n * prm->N);
+#pragma omp parallel for schedule(static) num_threads(prm->threads > 0 ? prm->threads : 1)
+    for (int i = 0; i < n; ++i) {
+        oracle::XorwowState rs;
+        memcpy(rs.v, &rng[6 * (size_t)i], 5 * sizeof(uint32_t));
+        rs.d = rng[6 * (size_t)i + 5];
+        float* x1 = &children[(size_t)i * SAMPLE_DIM];
+        const float* x0 = &parents[(size_t)i * SAMPLE_DIM];
+        const bool ok = prm->agent == 1 ? propagate_point(x0, x1, rs, pc) : propagate_car(x0, x1, rs, pc);
+        const int c1 = getR1(x1[0], x1[1], R1Size, prm->N);
+        const int c2 = getR2(x1[0], x1[1], c1, R1Size, prm->N, R2Size, prm->n);
+        uint8_t acc = 0;
+        if (ok && R1Score) {
+            const float u = oracle::xorwow_uniform(rs);   // KGMT.cu:395
+            acc = (c1 >= 0 && c2 >= 0 && (u <= R1Score[c1] || R2Avail[c2] == 0)) ? 1 : 0;
+        }
+        valid[i] = ok ? 1 : 0;
+        r1[i] = c1;
+        r2[i] = c2;
+        accept[i] = acc;
+        memcpy(&rng[6 * (size_t)i], rs.v, 5 * sizeof(uint32_t));
+        rng[6 * (size_t)i + 5] = rs.d;
+    }
+}
+
 void oracle_sincosf(const float* x, int n, float* s, float* c) {
     for (int i = 0; i < n; ++i) sbmp::sincosf_d(x[i], &s[i], &c[i]);
 }

@@ -89,6 +89,9 @@ void oracle_xorwow_draw(uint32_t state[6], int count, uint32_t* out);
 
 /* Invariant I1: re-propagate parents (n x 4) with stored controls (n x 3: a, steering,
  * duration) -> out (n x 4), valid (n).  Uses prm's agent, numDisc, agentLength, workspace. */
+void oracle_expand_batch(const oracle_params* prm, const float* obstacles, int nObs, const float* parents,
+                         uint32_t* rng, int n, const float* R1Score, const int* R2Avail, float* children,
+                         uint8_t* valid, int* r1, int* r2, uint8_t* accept);
 void oracle_replay(const oracle_params* prm, const float* obstacles, int nObs, const float* parents,
                    const float* controls, int n, float* out, uint8_t* valid);
 

@@ -88,6 +88,7 @@ def lib():
         L.oracle_xorwow_draw.argtypes = [vp, i, vp]
         L.oracle_replay.argtypes = [P(OracleParams), vp, i, vp, vp, i, vp, vp]
         L.oracle_sincosf.argtypes = [vp, i, vp, vp]
+        L.oracle_expand_batch.argtypes = [P(OracleParams), vp, i, vp, vp, i, vp, vp, vp, vp, vp, vp, vp]
         L.oracle_random_tree.argtypes = [i, vp, i, i, i, vp]
         L.oracle_tanf.argtypes = [vp, i, vp]
         _lib = L
@@ -246,6 +247,66 @@ def replay(cfg: PlannerConfig, obstacles, parents: np.ndarray, controls: np.ndar
     lib().oracle_replay(ctypes.byref(p), _fp(obs), len(obs) // 4, _fp(parents), _fp(controls), n, _fp(out),
                         _fp(valid))
     return out, valid.astype(bool)
+
+
+def expand_batch(cfg: PlannerConfig, obstacles, parents: np.ndarray, rng: np.ndarray, R1Score=None, R2Avail=None,
+                 threads: int = 8) -> dict:
+    """propagateG's per-child work over a batch (KGMT.cu:386-411): parents (n, 7), rng (n, 6)
+    uint32 XORWOW states -> children (n, 7), valid, r1, r2, accept (R1Score / R2Avail given)
+    and the advanced RNG states.  The checker of sbmp_expand_batch."""
+    p = OracleParams(cfg.width, cfg.height, cfg.N, cfg.n, cfg.numIterations, cfg.maxTreeSize, cfg.numDisc,
+                     cfg.agentLength, cfg.goalThreshold, cfg.samplesPerIteration, cfg.agent, cfg.fixGNewClear,
+                     threads, 1, 0, cfg.batchRule)
+    obs = np.ascontiguousarray(obstacles, dtype=np.float32).ravel()
+    par = np.ascontiguousarray(parents, dtype=np.float32)
+    st = np.ascontiguousarray(rng, dtype=np.uint32).copy()
+    n = len(par)
+    out = {"children": np.zeros((n, 7), dtype=np.float32), "valid": np.zeros(n, dtype=np.uint8),
+           "r1": np.zeros(n, dtype=np.int32), "r2": np.zeros(n, dtype=np.int32),
+           "accept": np.zeros(n, dtype=np.uint8)}
+    sc = None if R1Score is None else np.ascontiguousarray(R1Score, dtype=np.float32)
+    av = None if R2Avail is None else np.ascontiguousarray(R2Avail, dtype=np.int32)
+    lib().oracle_expand_batch(ctypes.byref(p), _fp(obs), len(obs) // 4, _fp(par), _fp(st), n,
+                              None if sc is None else _fp(sc), None if av is None else _fp(av),
+                              _fp(out["children"]), _fp(out["valid"]), _fp(out["r1"]), _fp(out["r2"]),
+                              _fp(out["accept"]))
+    out["rng"] = st
+    return out
+
+
+def insert_batch(gnew: np.ndarray, unexplored: np.ndarray, uParent: np.ndarray, samples: np.ndarray,
+                 parent: np.ndarray, costs: np.ndarray, treeSize: int, goal, goalThreshold: float,
+                 fixGNewClear: bool = False):
+    """updateG over a batch (KGMT.cu:221-249 exclusive_scan(GNew) + findInd + updateG, 540-593),
+    in place on copies: the accepted slots, in slot order, become rows treeSize + j with
+    parent uParent, cost = cost[parent] + duration (getCost, KGMT.cu:631-633); only
+    min(A, 32 floor(M/32)) rows are written (the updateG grid, KGMT.cu:231) and none past M
+    (D13); GNew[0 .. 32 min(A, M/32)) is cleared (D6; everything with fixGNewClear).
+    Returns (samples, parent, costs, gnew, A, lowest new row in the goal region or -1)."""
+    samples, parent, costs, gnew = samples.copy(), parent.copy(), costs.copy(), gnew.copy()
+    M = len(parent)
+    idx = np.nonzero(gnew)[0]
+    A = len(idx)
+    grid = min(A, M // 32)
+    nIns = min(A, 32 * grid)
+    goal_row = -1
+    for j in range(nIns):
+        dst = treeSize + j
+        if dst >= M:
+            break
+        s = idx[j]
+        parent[dst] = uParent[s]
+        samples[dst] = unexplored[s]
+        costs[dst] = np.float32(costs[uParent[s]] + unexplored[s, 6])
+        dx = np.float32(unexplored[s, 0] - np.float32(goal[0]))
+        dy = np.float32(unexplored[s, 1] - np.float32(goal[1]))
+        if goal_row < 0 and np.sqrt(np.float32(dx * dx + dy * dy), dtype=np.float32) < np.float32(goalThreshold):
+            goal_row = dst
+    if fixGNewClear:
+        gnew[:] = 0
+    else:
+        gnew[:32 * grid] = 0
+    return samples, parent, costs, gnew, A, goal_row
 
 
 def random_tree(kind: str, root, rows: int, blocks: int, tpb: int) -> np.ndarray:
