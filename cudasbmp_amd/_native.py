@@ -65,6 +65,11 @@ class HostCollectives(ctypes.Structure):
                 ("allgather", ALLGATHER_FN)]
 
 
+class SystemConfig(ctypes.Structure):   # sbmp_system_config
+    _fields_ = [("params", KgmtParams), ("initial", ctypes.c_float * 7), ("goal", ctypes.c_float * 7),
+                ("obstacles", ctypes.c_char * 1024)]
+
+
 class ExpandBatchArgs(ctypes.Structure):   # sbmp_expand_batch_args
     _fields_ = [("count", ctypes.c_int), ("parents", ctypes.c_void_p), ("rng", ctypes.c_void_p),
                 ("obstacles", ctypes.c_void_p), ("obstaclesCount", ctypes.c_int), ("agent", ctypes.c_int),
@@ -97,7 +102,8 @@ EXPORTED_SYMBOLS = (
     "sbmp_read_obstacles_csv", "sbmp_device_upload_f32", "sbmp_device_free",
     "sbmp_device_count", "sbmp_comm_get_unique_id", "sbmp_kgmt_create_sharded", "sbmp_kgmt_create_local_group",
     "sbmp_kgmt_create_sharded_host", "sbmp_expand_batch", "sbmp_expand_batch_host", "sbmp_insert_batch",
-    "sbmp_device_alloc", "sbmp_device_copy_to", "sbmp_device_copy_from",
+    "sbmp_device_alloc", "sbmp_device_copy_to", "sbmp_device_copy_from", "sbmp_kgmt_set_iteration_dump",
+    "sbmp_load_system_config",
     "sbmp_obstacle_grid_query", "sbmp_kgmt_solution_path", "sbmp_random_tree",
 )
 
@@ -124,6 +130,7 @@ def lib():
     L.sbmp_last_error.restype = ctypes.c_char_p
     sig = {
         "sbmp_kgmt_default_params": [P(KgmtParams)],
+        "sbmp_load_system_config": [ctypes.c_char_p, P(SystemConfig)],
         "sbmp_kgmt_create": [P(KgmtParams), P(vp)],
         "sbmp_kgmt_create_sharded": [P(KgmtParams), vp, i, i, P(vp)],
         "sbmp_kgmt_create_local_group": [P(KgmtParams), i, P(vp)],
@@ -152,6 +159,7 @@ def lib():
         "sbmp_kgmt_copy_rng": [vp, vp, i],
         "sbmp_kgmt_iter_log": [vp, vp, i, P(i)],
         "sbmp_kgmt_export_csv": [vp, ctypes.c_char_p],
+        "sbmp_kgmt_set_iteration_dump": [vp, ctypes.c_char_p],
         "sbmp_kgmt_kernel_stats": [vp, vp, i, P(i)],
         "sbmp_kgmt_reset_kernel_stats": [vp],
         "sbmp_kgmt_set_profiling": [vp, i],

@@ -1,17 +1,20 @@
-"""System / workspace configuration.
+"""System / workspace configuration (SURVEY.md §8f-2).
 
 The reference hardcodes everything in demos/main.cu:19-46 and ships an empty
 systems/car.yaml (yaml-cpp is linked but never called, CMakeLists.txt:10,47).
-This module reads systems/*.yaml (populated from main.cu's constants) so a
-configuration can be selected without recompiling.
+systems/*.yaml hold those constants and the benchmark workloads c1-c5; they are
+read by the library's own parser (sbmp_load_system_config, csrc/config.cpp), the
+same one the C++ demo and facade use, so Python needs no YAML package.
 """
 from __future__ import annotations
 
+import ctypes
 import os
 
-import yaml
+from . import _native as nat
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SYSTEMS = os.path.join(ROOT, "systems")
 
 # reference demos/main.cu:33-45
 DEMO_INITIAL = (5.0, 5.0, 0.0, 0.0, 0.0, 0.0, 0.0)
@@ -21,21 +24,25 @@ PLANNER_KEYS = ("width", "height", "N", "n", "numIterations", "maxTreeSize", "nu
                 "goalThreshold")
 
 
-def load_system_config(path: str = os.path.join(ROOT, "systems", "car.yaml")) -> dict:
-    """Return {'planner': ctor kwargs, 'agent', 'initial', 'goal', 'obstacles' (path)}."""
-    with open(path) as f:
-        raw = yaml.safe_load(f) or {}
-    missing = [k for k in PLANNER_KEYS if k not in raw]
-    if missing:
-        raise ValueError(f"{path}: missing keys {missing}")
-    base = os.path.dirname(os.path.abspath(path))
-    obstacles = raw.get("obstacles")
-    if obstacles and not os.path.isabs(obstacles):
-        obstacles = os.path.normpath(os.path.join(base, obstacles))
+def load_system_config(path: str = os.path.join(SYSTEMS, "car.yaml")) -> dict:
+    """Return {'planner': KGMT ctor kwargs, 'agent', 'samplesPerIteration', 'batchRule',
+    'fixGNewClear', 'initial', 'goal', 'obstacles' (resolved path or None)}."""
+    c = nat.SystemConfig()
+    nat.call("sbmp_load_system_config", os.fspath(path).encode(), ctypes.byref(c))
+    p = c.params
+    obstacles = c.obstacles.decode()
     return {
-        "planner": {k: raw[k] for k in PLANNER_KEYS},
-        "agent": raw.get("agent", "car"),
-        "initial": tuple(float(v) for v in raw.get("initial", DEMO_INITIAL)),
-        "goal": tuple(float(v) for v in raw.get("goal", DEMO_GOAL)),
-        "obstacles": obstacles,
+        "planner": {k: getattr(p, k) for k in PLANNER_KEYS},
+        "agent": "point" if p.agent == nat.SBMP_AGENT_POINT else "car",
+        "samplesPerIteration": p.samplesPerIteration,
+        "batchRule": "fill" if p.batchRule == nat.SBMP_BATCH_FILL else "reference",
+        "fixGNewClear": bool(p.fixGNewClear),
+        "initial": tuple(float(v) for v in c.initial),
+        "goal": tuple(float(v) for v in c.goal),
+        "obstacles": obstacles or None,
     }
+
+
+def workload(name: str) -> dict:
+    """The benchmark workload systems/<name>.yaml (c1-c5, BASELINE.json configs)."""
+    return load_system_config(os.path.join(SYSTEMS, f"{name}.yaml"))

@@ -497,6 +497,20 @@ bool KgmtPlanner::active() {
 }
 
 void Planner::run(int pollEvery) {
+    if (!dumpDir_.empty()) {   // one iteration at a time, dumping each (KGMT.cu:263-290)
+        int done = 0;
+        while (true) {
+            enqueue(1);
+            sync();
+            const std::vector<sbmp_iter_record> log = iter_log();
+            for (const sbmp_iter_record& e : log)
+                if (e.itr > done) dump_iteration(dumpDir_, e.itr);
+            if (!log.empty()) done = log.back().itr;
+            if (!active()) break;
+        }
+        sync();
+        return;
+    }
     if (pollEvery < 1) pollEvery = 1;
     while (true) {
         enqueue(pollEvery);
@@ -747,6 +761,33 @@ void KgmtPlanner::copy_r2_partial(int* R2Valid, int* R2Invalid) {
     sync();
     SBMP_HIP(hipMemcpy(R2Valid, d_.R2Valid, sizeof(int) * d_.nR2, hipMemcpyDeviceToHost));
     SBMP_HIP(hipMemcpy(R2Invalid, d_.R2Invalid, sizeof(int) * d_.nR2, hipMemcpyDeviceToHost));
+}
+
+// The per-iteration dumps of KGMT.cu:263-290 (the reference creates Data/G and
+// Data/GNew as well but writes nothing there).  State as at the end of iteration itr:
+// tree, parents and the unexplored buffer after its insertion, R1 / R1Avail with its
+// children counted, the R1Score its accept test used.
+void Planner::dump_iteration(const std::string& dir, int itr) {
+    const sbmp_kgmt_params& p = params();
+    const size_t M = p.maxTreeSize, n1 = (size_t)p.N * p.N, n2 = n1 * p.n * p.n;
+    const std::string base = (dir.empty() ? std::string(".") : dir) + "/Data";
+    mkdir((dir.empty() ? std::string(".") : dir).c_str(), 0755);
+    mkdir(base.c_str(), 0755);
+    for (const char* k : {"Samples", "UnexploredSamples", "Parents", "R1Scores", "R1Avail", "R1", "G", "GNew"})
+        mkdir((base + "/" + k).c_str(), 0755);
+    std::vector<float> samples(M * 7), costs(M), uS(M * 7), score(n1);
+    std::vector<int> parent(M), uP(M), R1(n1), R1A(n1);
+    copy_tree(samples.data(), parent.data(), costs.data());
+    copy_unexplored(uS.data(), uP.data());
+    copy_regions(R1.data(), R1A.data(), nullptr, nullptr, score.data(), nullptr, nullptr, nullptr);
+    const std::string i = std::to_string(itr);
+    write_csv(base + "/Samples/samples" + i + ".csv", samples.data(), M, 7);
+    write_csv(base + "/Parents/parents" + i + ".csv", parent.data(), M, 1);
+    write_csv(base + "/R1Scores/R1Scores" + i + ".csv", score.data(), n1, 1);
+    write_csv(base + "/R1Avail/R1Avail" + i + ".csv", R1A.data(), n1, 1);
+    write_csv(base + "/R1/R1" + i + ".csv", R1.data(), n1, 1);
+    write_csv(base + "/UnexploredSamples/unexploredSamples" + i + ".csv", uS.data(), M, 7);
+    (void)n2;
 }
 
 void Planner::export_csv(const std::string& dir) {

@@ -49,6 +49,11 @@ public:
     virtual bool active() = 0;   // syncs; false once the loop has ended
     virtual void result(sbmp_plan_result* r) = 0;
     void run(int pollEvery);     // enqueue until the loop ends
+    // Per-iteration dumps (reference KGMT.cu:263-290, commented out there; read by
+    // visualization/visualizationKGMT_Steps.m): with a directory set, run() steps one
+    // iteration at a time and writes <dir>/Data/<Kind>/<kind><itr>.csv after each.
+    void set_iteration_dump(const std::string& dir) { dumpDir_ = dir; }
+    void dump_iteration(const std::string& dir, int itr);
 
     virtual hipStream_t stream() const = 0;
     virtual int num_slots() const = 0;
@@ -72,6 +77,9 @@ public:
     virtual void set_profiling(bool on) = 0;
     virtual void enqueue_delay(double us) = 0;
     virtual std::vector<float> kernel_samples(const std::string& name) = 0;
+
+protected:
+    std::string dumpDir_;
 };
 
 // Legacy random-tree generators (random_tree.hip): rows x (blocks * tpb) samples

@@ -27,6 +27,7 @@ void comm_get_unique_id(uint8_t* id);
 void expand_batch(const sbmp_expand_batch_args* args, void* stream);   // batch.hip
 void expand_batch_host(const sbmp_expand_batch_args* args);
 void insert_batch(const sbmp_insert_batch_args* args, void* stream);
+void load_system_config(const char* path, sbmp_system_config* out);   // config.cpp
 }  // namespace sbmp
 
 static thread_local std::string g_last_error;
@@ -93,6 +94,10 @@ sbmp_status sbmp_kgmt_default_params(sbmp_kgmt_params* p) {
         p->device = 0;
         p->profileKernels = 0;
     });
+}
+
+sbmp_status sbmp_load_system_config(const char* path, sbmp_system_config* out) {
+    return guarded([&] { sbmp::load_system_config(path, out); });
 }
 
 sbmp_status sbmp_kgmt_create(const sbmp_kgmt_params* p, sbmp_kgmt** out) {
@@ -241,6 +246,13 @@ sbmp_status sbmp_kgmt_sync(sbmp_kgmt* h) {
     return guarded([&] {
         PLANNER(h);
         P.sync();
+    });
+}
+
+sbmp_status sbmp_kgmt_set_iteration_dump(sbmp_kgmt* h, const char* dir) {
+    return guarded([&] {
+        PLANNER(h);
+        P.set_iteration_dump(dir ? std::string(dir) : std::string());
     });
 }
 

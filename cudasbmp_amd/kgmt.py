@@ -301,6 +301,10 @@ class KGMT:
         """The 13 CSV dumps of KGMT.cu:299-311."""
         nat.call("sbmp_kgmt_export_csv", self._h, directory.encode())
 
+    def set_iteration_dump(self, directory: Optional[str]) -> None:
+        """Per-iteration Data/<Kind>/<kind><itr>.csv dumps during plan() (KGMT.cu:263-290); None: off."""
+        nat.call("sbmp_kgmt_set_iteration_dump", self._h, directory.encode() if directory else None)
+
     def kernel_stats(self) -> dict:
         cnt = ctypes.c_int()
         arr = (nat.KernelStat * 16)()

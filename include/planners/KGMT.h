@@ -60,8 +60,21 @@ public:
         params_.goalThreshold = goalThreshold;
         SBMP_CHECK(sbmp_kgmt_create(&params_, &h_));
     }
+    // Build extension: every planner parameter, e.g. from a system file (loadConfig).
+    explicit KGMT(const sbmp_kgmt_params& p)
+        : numIterations_(p.numIterations), maxTreeSize_(p.maxTreeSize), numDisc_(p.numDisc), treeSize_(0),
+          width_(p.width), height_(p.height), costToGoal_(0.0f), agentLength_(p.agentLength), R1Threshold_(0.0f),
+          goalThreshold_(p.goalThreshold), params_(p) {
+        SBMP_CHECK(sbmp_kgmt_create(&params_, &h_));
+    }
     ~KGMT() {
         if (h_) sbmp_kgmt_destroy(h_);
+    }
+    // systems/*.yaml (the reference hardcodes these in main.cu:19-46).
+    static sbmp_system_config loadConfig(const char* path) {
+        sbmp_system_config c;
+        SBMP_CHECK(sbmp_load_system_config(path, &c));
+        return c;
     }
     KGMT(const KGMT&) = delete;
     KGMT& operator=(const KGMT&) = delete;
@@ -89,6 +102,9 @@ public:
         explicitSeed_ = true;
     }
     void setWriteCsv(bool on) { writeCsv_ = on; }
+    // The per-iteration Data/<Kind>/<kind><itr>.csv dumps of KGMT.cu:263-290 (commented
+    // out in the reference); nullptr: off.
+    void dumpIterations(const char* dir) { SBMP_CHECK(sbmp_kgmt_set_iteration_dump(h_, dir)); }
     const sbmp_plan_result& result() const { return result_; }
     // Path root .. solution node: tree rows and their 7-float
     // samples; empty if plan() found no solution.

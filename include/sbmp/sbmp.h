@@ -104,6 +104,21 @@ const char* sbmp_last_error(void);
 /* The demo configuration, reference demos/main.cu:19-28. */
 sbmp_status sbmp_kgmt_default_params(sbmp_kgmt_params* p);
 
+/* A system / workspace file (systems/NAME.yaml): the reference hardcodes
+ * this in demos/main.cu:19-46 and leaves systems/car.yaml empty.  Flat "key: value"
+ * lines over the demo defaults: agent, width, height, N, n, numIterations, maxTreeSize,
+ * numDisc, agentLength, goalThreshold, samplesPerIteration, batchRule (reference | fill),
+ * fixGNewClear, device, initial / goal ([7 values] or a CSV file such as
+ * configurations/init/init.csv), obstacles (a CSV path, resolved against the file's
+ * directory).  Numeric keys may name a file holding the number.  Unknown keys fail. */
+typedef struct sbmp_system_config {
+    sbmp_kgmt_params params;
+    float initial[7];
+    float goal[7];
+    char obstacles[1024];     /* resolved path, "" if the file names none */
+} sbmp_system_config;
+sbmp_status sbmp_load_system_config(const char* path, sbmp_system_config* out);
+
 /* KGMT::KGMT (KGMT.cu:10-78): allocates every planner buffer on p->device. */
 sbmp_status sbmp_kgmt_create(const sbmp_kgmt_params* p, sbmp_kgmt** out);
 sbmp_status sbmp_kgmt_destroy(sbmp_kgmt* h);
@@ -150,6 +165,13 @@ sbmp_status sbmp_kgmt_copy_rng(sbmp_kgmt* h, uint32_t* states, int capacity);
 sbmp_status sbmp_kgmt_iter_log(sbmp_kgmt* h, sbmp_iter_record* out, int capacity, int* count);
 /* The 13 CSV dumps of KGMT.cu:299-311 (std::fixed, 10 decimals, helper.cuh:53-72) into dir. */
 sbmp_status sbmp_kgmt_export_csv(sbmp_kgmt* h, const char* dir);
+/* The per-iteration dumps the reference has commented out (KGMT.cu:263-290), read by
+ * visualization/visualizationKGMT_Steps.m: with dir set, sbmp_kgmt_plan runs one
+ * iteration at a time (one host sync each) and after iteration itr writes
+ * dir/Data/{Samples/samples, Parents/parents, R1Scores/R1Scores, R1Avail/R1Avail,
+ * R1/R1, UnexploredSamples/unexploredSamples}<itr>.csv in the export format.
+ * dir NULL or "": off (the default). */
+sbmp_status sbmp_kgmt_set_iteration_dump(sbmp_kgmt* h, const char* dir);
 
 /* Solution path (the reference keeps only the goal node's cost,
  * KGMT.cu:586-591): the tree rows from the root to `node` (node < 0: the
