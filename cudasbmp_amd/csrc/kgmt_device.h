@@ -481,7 +481,7 @@ __device__ __forceinline__ bool propagate_car(float4 p, Xorwow& rs, const KgmtDe
         bool freeSeg;
         if (OBS >= kObsReg) freeSeg = motion_valid_culled<OBS>(minx, miny, maxx, maxy, obs, cull.boxes);
         else if (OBS == kObsGrid)   // only lanes whose result counts walk their cells
-            freeSeg = oob || grid_motion_valid(minx, miny, maxx, maxy, d.gridG, d.gridInvW, d.gridInvH,
+            freeSeg = oob || grid_motion_valid_batched(minx, miny, maxx, maxy, d.gridG, d.gridInvW, d.gridInvH,
                                                d.gridStart, d.gridBoxes);
         else freeSeg = motion_valid<OBS>(minx, miny, maxx, maxy, obs, d.nObs);
         x = nx;
@@ -524,7 +524,7 @@ __device__ __forceinline__ bool propagate_point(float4 p, Xorwow& rs, const Kgmt
         bool freeSeg;
         if (OBS >= kObsReg) freeSeg = motion_valid_culled<OBS>(minx, miny, maxx, maxy, obs, cull.boxes);
         else if (OBS == kObsGrid)
-            freeSeg = oob || grid_motion_valid(minx, miny, maxx, maxy, d.gridG, d.gridInvW, d.gridInvH,
+            freeSeg = oob || grid_motion_valid_batched(minx, miny, maxx, maxy, d.gridG, d.gridInvW, d.gridInvH,
                                                d.gridStart, d.gridBoxes);
         else freeSeg = motion_valid<OBS>(minx, miny, maxx, maxy, obs, d.nObs);
         x = nx;

@@ -65,4 +65,55 @@ SBMP_HD bool grid_motion_valid(float minx, float miny, float maxx, float maxy, i
     return true;
 }
 
+#if defined(__HIPCC__)
+// Device form of grid_motion_valid with the same answer (an OR over the listed
+// boxes, so the order of the tests does not matter): the start offsets of the
+// segment's cell rows are loaded together, and the boxes of a row in groups of
+// eight, all eight loads issued before any test, instead of one dependent global
+// load per box with an early exit after each (a chain of L2 round trips per Euler
+// step, which bounded the dense c5 field).
+__device__ __forceinline__ bool grid_motion_valid_batched(float minx, float miny, float maxx, float maxy, int g,
+                                                          float invW, float invH, const int* __restrict__ start,
+                                                          const float4* __restrict__ boxes) {
+    const int cx0 = grid_cell(minx, invW, g), cx1 = grid_cell(maxx, invW, g);
+    const int cy0 = grid_cell(miny, invH, g), cy1 = grid_cell(maxy, invH, g);
+    constexpr int kRows = 2;   // a step's segment spans one or two cell rows almost always
+    constexpr int kBatch = 8;  // boxes loaded per round trip (a row of a few cells lists ~4-14 at c5's density)
+    int b[kRows], e[kRows];
+#pragma unroll
+    for (int r = 0; r < kRows; ++r) {
+        const int cy = min(cy0 + r, cy1);
+        b[r] = start[cy * g + cx0];
+        e[r] = start[cy * g + cx1 + 1];
+        if (cy0 + r > cy1) e[r] = b[r];
+    }
+    bool hit = false;
+    for (int cy = cy0; cy <= cy1 && !hit; cy += kRows) {
+        if (cy > cy0) {   // rows beyond the first pair (a long segment): reload
+#pragma unroll
+            for (int r = 0; r < kRows; ++r) {
+                const int c = min(cy + r, cy1);
+                b[r] = start[c * g + cx0];
+                e[r] = start[c * g + cx1 + 1];
+                if (cy + r > cy1) e[r] = b[r];
+            }
+        }
+#pragma unroll
+        for (int r = 0; r < kRows; ++r) {
+            for (int i = b[r]; i < e[r] && !hit; i += kBatch) {
+                const int last = e[r] - 1;
+                float4 o[kBatch];
+#pragma unroll
+                for (int k = 0; k < kBatch; ++k) o[k] = boxes[min(i + k, last)];
+                // a repeated last box (fewer than kBatch left in the row) is tested twice: same answer
+#pragma unroll
+                for (int k = 0; k < kBatch; ++k)
+                    hit |= !((maxx <= o[k].x) || (o[k].z <= minx) || (maxy <= o[k].y) || (o[k].w <= miny));
+            }
+        }
+    }
+    return !hit;
+}
+#endif
+
 }  // namespace sbmp
