@@ -410,6 +410,7 @@ __device__ __forceinline__ WaveCull wave_cull(float x0, float y0, float rx, floa
 template <int OBS>
 __device__ __forceinline__ bool motion_valid_culled(float minx, float miny, float maxx, float maxy,
                                                     const float4* __restrict__ obs, unsigned boxes) {
+    if (boxes == 0u) return true;   // uniform: the common case skips every test
     bool hit = false;
 #pragma unroll
     for (int i = 0; i < obs_in_registers(OBS); ++i)
@@ -432,7 +433,7 @@ struct NoMidHook {
     __device__ void operator()() const {}
 };
 
-// midHook() runs once, at Euler step numDisc / 2, on every lane that entered (k_step
+// midHook() runs once, before Euler step numDisc / 2, on every lane that entered (k_step
 // issues the planner-publication loads there: late enough to see them, early enough
 // that they have landed when propagation ends).
 template <int OBS, typename MidHook = NoMidHook>
@@ -443,7 +444,10 @@ __device__ __forceinline__ bool propagate_car(float4 p, Xorwow& rs, const KgmtDe
     const float steering = (float)__builtin_fma((double)(u2 * 2.0f), 3.141592653589793, -3.141592653589793);
     const float duration = __builtin_fmaf(xorwow_uniform(rs), 1.0f, 0.05f);
     const float dt = div_or_ieee(duration, (float)d.numDisc, d.rcpNumDisc);
-    float x = p.x, y = p.y, theta = p.z, v = p.w;
+    // (x, y) and (theta, v) as float pairs: each pair update is one v_pk_mul_f32 /
+    // v_pk_fma_f32 doing the same IEEE operation per component (same bits).
+    sbmp_f32x2 xy = {p.x, p.y}, tv = {p.z, p.w};
+    const sbmp_f32x2 dt2 = {dt, dt};
     const float tan_steering = tanf_d(steering);
     // |v| <= |v0| + |a| t, so the displacement stays below T |v0| + |a| T^2 / 2.
     WaveCull cull{~0u, true};
@@ -452,16 +456,15 @@ __device__ __forceinline__ bool propagate_car(float4 p, Xorwow& rs, const KgmtDe
         cull = wave_cull<OBS>(p.x, p.y, r, r, obs, d);
     }
     bool alive = true;
-    const int midStep = d.numDisc >> 1;
-    for (int i = 0; i < d.numDisc; ++i) {
-        if (i == midStep) midHook();   // uniform
-        if (!alive) continue;
+    auto step = [&]() {
+        if (!alive) return;
         float st, ct;
-        sincos_pred(theta, &st, &ct);
-        const float nx = __builtin_fmaf(v * ct, dt, x);
-        const float ny = __builtin_fmaf(v * st, dt, y);
+        sincos_pred(tv.x, &st, &ct);
+        const sbmp_f32x2 nxy = __builtin_elementwise_fma(sbmp_f32x2{tv.y, tv.y} * sbmp_f32x2{ct, st}, dt2, xy);
+        const float nx = nxy.x, ny = nxy.y;
         // min(nx, ny) <= 0 is (nx <= 0) | (ny <= 0) for finite operands (D15)
         const bool oob = cull.bounds && ((seg_min(nx, ny) <= 0.0f) | (nx >= d.width) | (ny >= d.height));
+        const float v = tv.y;
         float vl;
         if (d.invAgentLength != 0.0f) {
             vl = v * d.invAgentLength;
@@ -471,27 +474,29 @@ __device__ __forceinline__ bool propagate_car(float4 p, Xorwow& rs, const KgmtDe
                               !(__builtin_fabsf(v) <= 0x1p100f);
             if (__ballot(slow) != 0ull && slow) vl = v / d.agentLength;
         }
-        const float nth = __builtin_fmaf(vl * tan_steering, dt, theta);
-        const float nv = __builtin_fmaf(a, dt, v);
+        // (theta + vl tan dt, v + a dt): KGMT statePropagator.cu's two updates as one pair
+        const sbmp_f32x2 ntv = __builtin_elementwise_fma(sbmp_f32x2{vl * tan_steering, a}, dt2, tv);
         // (x > nx ? nx : x) etc. as one v_min / v_max.  They differ from the ternaries
         // only for NaN operands, which need a non-finite theta or v: begin() rejects a
         // non-finite root, and finite states stay finite.
-        const float minx = seg_min(x, nx), maxx = seg_max(x, nx);
-        const float miny = seg_min(y, ny), maxy = seg_max(y, ny);
+        const float minx = seg_min(xy.x, nx), maxx = seg_max(xy.x, nx);
+        const float miny = seg_min(xy.y, ny), maxy = seg_max(xy.y, ny);
         bool freeSeg;
         if (OBS >= kObsReg) freeSeg = motion_valid_culled<OBS>(minx, miny, maxx, maxy, obs, cull.boxes);
         else if (OBS == kObsGrid)   // only lanes whose result counts walk their cells
             freeSeg = oob || grid_motion_valid_batched(minx, miny, maxx, maxy, d.gridG, d.gridInvW, d.gridInvH,
                                                d.gridStart, d.gridBoxes);
         else freeSeg = motion_valid<OBS>(minx, miny, maxx, maxy, obs, d.nObs);
-        x = nx;
-        y = ny;
-        if (!oob) {
-            theta = nth;
-            v = nv;
-        }
+        xy = nxy;
+        if (!oob) tv = ntv;
         alive = !oob & freeSeg;
-    }
+    };
+    // two loops around the hook: no per-step test of the step index
+    const int midStep = d.numDisc >> 1;
+    for (int i = 0; i < midStep; ++i) step();
+    midHook();
+    for (int i = midStep; i < d.numDisc; ++i) step();
+    const float x = xy.x, y = xy.y, theta = tv.x, v = tv.y;
     out.state = make_float4(x, y, theta, v);
     out.a = a;
     out.steer = steering;
@@ -512,10 +517,8 @@ __device__ __forceinline__ bool propagate_point(float4 p, Xorwow& rs, const Kgmt
     if (OBS >= kObsReg)
         cull = wave_cull<OBS>(p.x, p.y, duration * __builtin_fabsf(vx), duration * __builtin_fabsf(vy), obs, d);
     bool alive = true;
-    const int midStep = d.numDisc >> 1;
-    for (int i = 0; i < d.numDisc; ++i) {
-        if (i == midStep) midHook();   // uniform
-        if (!alive) continue;
+    auto step = [&]() {
+        if (!alive) return;
         const float nx = __builtin_fmaf(vx, dt, x);
         const float ny = __builtin_fmaf(vy, dt, y);
         const bool oob = cull.bounds && ((seg_min(nx, ny) <= 0.0f) | (nx >= d.width) | (ny >= d.height));
@@ -530,7 +533,11 @@ __device__ __forceinline__ bool propagate_point(float4 p, Xorwow& rs, const Kgmt
         x = nx;
         y = ny;
         alive = !oob & freeSeg;
-    }
+    };
+    const int midStep = d.numDisc >> 1;
+    for (int i = 0; i < midStep; ++i) step();
+    midHook();
+    for (int i = midStep; i < d.numDisc; ++i) step();
     out.state = make_float4(x, y, 0.0f, 0.0f);
     out.a = vx;
     out.steer = vy;
