@@ -760,6 +760,64 @@ __global__ __launch_bounds__(kBlock) void k_finish(KgmtDev d, int t) {
     }
 }
 
+// ------------------------------------------------------------------ one-shot exchange
+// recv = sum over ranks of send, through inboxes mapped with HIP IPC, in place of the
+// RCCL all-reduce of the exchange buffer.  Every rank's inbox is
+// [2 parities][nranks slots][n words] followed by flags[nranks][kOneshotChunks].
+// Workgroup c owns chunk c of the words: it stores the chunk into slot `rank` of every
+// rank's inbox (parity seq & 1) with system-scope stores, fences, raises its flag
+// (seq) at every rank, waits for every rank's flag of chunk c in its own inbox, and
+// sums the chunk's slots.  seq counts the exchanges of the plan's lifetime and is the
+// same on every rank; a rank is at most one exchange ahead of another (it waits for
+// the other's flags), so it writes parity seq & 1 only after every reader of exchange
+// seq - 2 has summed it.
+constexpr int kOneshotChunks = 8;
+struct OneshotArgs {
+    unsigned long long* inbox[kMaxRanks];
+};
+__global__ __launch_bounds__(kBlock) void k_oneshot(OneshotArgs a, const unsigned long long* __restrict__ send,
+                                                    unsigned long long* __restrict__ recv, long long n, int nranks,
+                                                    int rank, unsigned long long seq, int* error) {
+    const int c = blockIdx.x;
+    const long long per = (n + kOneshotChunks - 1) / kOneshotChunks;
+    const long long lo = c * per, hi = min(n, lo + per);
+    const size_t par = (size_t)(seq & 1ull) * nranks * n;
+    const size_t flags = (size_t)2 * nranks * n;
+    for (long long i = lo + threadIdx.x; i < hi; i += kBlock) {
+        const unsigned long long v = send[i];
+        for (int q = 0; q < nranks; ++q)
+            __hip_atomic_store(a.inbox[q] + par + (size_t)rank * n + i, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+    __threadfence_system();   // this thread's stores reach every rank before the flag
+    __syncthreads();
+    const int q = threadIdx.x;
+    if (q < nranks) {
+        __hip_atomic_store(a.inbox[q] + flags + (size_t)rank * kOneshotChunks + c, seq, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+        unsigned long long* f = a.inbox[rank] + flags + (size_t)q * kOneshotChunks + c;
+        const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
+        while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < seq) {
+            if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > 100000000ll) {   // 1 s: report, do not hang
+                atomicExch(error, 1);
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+    }
+    __threadfence_system();
+    __syncthreads();
+    for (long long i = lo + threadIdx.x; i < hi; i += kBlock) {
+        unsigned long long sum = 0ull;
+        for (int r = 0; r < nranks; ++r)
+            sum += __hip_atomic_load(a.inbox[rank] + par + (size_t)r * n + i, __ATOMIC_RELAXED,
+                                     __HIP_MEMORY_SCOPE_SYSTEM);
+        recv[i] = sum;
+    }
+}
+
+size_t oneshot_inbox_words(long long n, int nranks) { return (size_t)2 * nranks * n + (size_t)nranks * kOneshotChunks; }
+
+
 // ------------------------------------------------------------------ step
 // k_step(t): one launch per iteration on a single rank, doing what
 // k_finish(t-1) and k_expand(t) do without the launch between them.
@@ -1580,6 +1638,14 @@ void launch_fold_r2(const KgmtDev& d, int tFirst, int tLast, hipStream_t s, cons
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
     const dim3 grid((d.logSlots + kFoldKeys - 1) / kFoldKeys, tLast - tFirst + 1);
     launch(k_fold_r2, grid, dim3(1024), shm, s, tm, d, tFirst);
+}
+
+void launch_oneshot(unsigned long long* const* inbox, const unsigned long long* send, unsigned long long* recv,
+                    long long n, int nranks, int rank, unsigned long long seq, int* error, hipStream_t s,
+                    const KernelTiming& tm) {
+    OneshotArgs a{};
+    for (int q = 0; q < nranks; ++q) a.inbox[q] = inbox[q];
+    launch(k_oneshot, dim3(kOneshotChunks), dim3(kBlock), 0, s, tm, a, send, recv, n, nranks, rank, seq, error);
 }
 
 void launch_finish(const KgmtDev& d, int t, int insertBlocks, hipStream_t s, const KernelTiming& tm) {

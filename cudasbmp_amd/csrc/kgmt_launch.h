@@ -32,6 +32,13 @@ void launch_finish(const KgmtDev& d, int t, int insertBlocks, hipStream_t s,
                    const KernelTiming& tm = KernelTiming());
 // Sharded ranks: pack this rank's accepted children of iteration t (blocks = owned blocks).
 void launch_pack(const KgmtDev& d, int t, int blocks, hipStream_t s, const KernelTiming& tm = KernelTiming());
+// Sharded ranks: recv = sum over ranks of send through IPC-mapped inboxes (inbox[q] =
+// rank q's, oneshot_inbox_words() u64 each, zeroed once); seq = this exchange's number
+// in the plan's lifetime (1, 2, ...), the same on every rank.
+size_t oneshot_inbox_words(long long n, int nranks);
+void launch_oneshot(unsigned long long* const* inbox, const unsigned long long* send, unsigned long long* recv,
+                    long long n, int nranks, int rank, unsigned long long seq, int* error, hipStream_t s,
+                    const KernelTiming& tm = KernelTiming());
 // Local shard group: recv[q][i] = sum over ranks of send[r][i], for every rank q.
 void launch_xsum(const unsigned long long* const* send, unsigned long long* const* recv, int nranks, long long n,
                  hipStream_t s);

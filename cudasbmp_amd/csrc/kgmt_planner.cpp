@@ -266,6 +266,19 @@ KgmtPlanner::KgmtPlanner(const sbmp_kgmt_params& p, int nranks, int rank, Exchan
         void* peers[kMaxRanks] = {nullptr};
         ex_->share_buffer(d.recOut, sizeof(float4) * 2 * kRecordF4 * (size_t)d.recCap, peers);
         for (int q = 0; q < nranks; ++q) d.recPeer[q] = static_cast<const float4*>(peers[q]);
+        // The per-iteration exchange: a one-shot sum through IPC-mapped inboxes (the
+        // default), or SBMP_EXCHANGE=collective for the Exchange's all-reduce (RCCL).
+        const char* v = getenv("SBMP_EXCHANGE");
+        if (!(v && std::string(v) == "collective")) {
+            const size_t words = oneshot_inbox_words((long long)xWords_, nranks);
+            unsigned long long* own = alloc<unsigned long long>(words);
+            SBMP_HIP(hipMemset(own, 0, sizeof(unsigned long long) * words));
+            SBMP_HIP(hipDeviceSynchronize());   // zeroed before any peer can see it
+            void* ib[kMaxRanks] = {nullptr};
+            ex_->share_buffer(own, sizeof(unsigned long long) * words, ib);
+            for (int q = 0; q < nranks; ++q) inbox_[q] = static_cast<unsigned long long*>(ib[q]);
+            oneshot_ = true;
+        }
     }
 }
 
@@ -421,7 +434,14 @@ void KgmtPlanner::stage_expand(int t) {
 void KgmtPlanner::stage_pack(int t) { launch_pack(d_, t, expandBlocks_, stream_, timing(K_PACK)); }
 
 void KgmtPlanner::stage_exchange() {
-    if (ex_) ex_->allreduce_u64(xSend_, xRecv_, xWords_, stream_);
+    if (!ex_) return;
+    if (oneshot_) {
+        ++xSeq_;
+        launch_oneshot(inbox_, xSend_, xRecv_, (long long)xWords_, d_.nranks, d_.rank, xSeq_, &d_.status->error,
+                       stream_, timing(K_XCHG));
+    } else {
+        ex_->allreduce_u64(xSend_, xRecv_, xWords_, stream_);
+    }
 }
 
 void KgmtPlanner::stage_finish(int t) {
@@ -850,7 +870,7 @@ void KgmtPlanner::collect_events() {
     pending_.clear();
 }
 
-static const char* kKernelNames[] = {"k_expand", "k_finish", "k_fold_r2", "k_pack", "k_step"};
+static const char* kKernelNames[] = {"k_expand", "k_finish", "k_fold_r2", "k_pack", "k_step", "k_oneshot"};
 
 std::vector<float> KgmtPlanner::kernel_samples(const std::string& name) {
     collect_events();

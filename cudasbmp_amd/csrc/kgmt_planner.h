@@ -143,7 +143,7 @@ public:
     int rank() const { return d_.rank; }
 
 private:
-    enum KernelId { K_EXPAND = 0, K_FINISH, K_FOLD, K_PACK, K_STEP, K_COUNT };
+    enum KernelId { K_EXPAND = 0, K_FINISH, K_FOLD, K_PACK, K_STEP, K_XCHG, K_COUNT };
     KernelTiming timing(int id);
     void collect_events();
     void read_ctrl(std::vector<IterCtrl>& c, PlannerStatus& st);
@@ -169,6 +169,9 @@ private:
     unsigned long long* xSend_ = nullptr;
     unsigned long long* xRecv_ = nullptr;
     size_t xWords_ = 0;
+    bool oneshot_ = false;                   // sharded: the exchange is k_oneshot over IPC-mapped inboxes
+    unsigned long long* inbox_[kMaxRanks] = {nullptr};
+    unsigned long long xSeq_ = 0;            // exchanges so far (the same count on every rank)
     uint32_t* jumps_ = nullptr;
     float4* obs_ = nullptr;
     int obsCap_ = 0;

@@ -4,8 +4,11 @@ Each process is one rank of sbmp_kgmt_create_sharded_host: the real k_expand /
 k_pack / k_finish kernels, record buffers written with system-scope stores and
 read by the peer over HIP IPC (hipIpcGetMemHandle / hipIpcOpenMemHandle, handles
 exchanged by an allgather), and the fused exchange buffer all-reduced every
-iteration.  Only RCCL is replaced: RCCL cannot put two ranks on one device, so the
-all-reduce runs over torch.distributed gloo through the host-collectives seam
+iteration, either by the default one-shot kernel (k_oneshot: each rank stores its
+buffer into every rank's IPC-mapped inbox and raises flags; both processes' kernels
+meet on the GPU) or, with SBMP_EXCHANGE=collective, by the Exchange's all-reduce.
+RCCL cannot put two ranks on one device, so that all-reduce and the IPC handle
+exchange run over torch.distributed gloo through the host-collectives seam
 (cudasbmp_amd/host_comm.py).  The ranks' merged state must equal the CPU oracle's
 single-rank run bit for bit.
 """
@@ -29,9 +32,13 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _rank_main(rank, port, kw, seed, out_dir):
+def _rank_main(rank, port, kw, seed, out_dir, exchange):
     import sys
     sys.path.insert(0, ROOT)
+    if exchange == "collective":
+        os.environ["SBMP_EXCHANGE"] = "collective"
+    else:
+        os.environ.pop("SBMP_EXCHANGE", None)
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     import torch.distributed as dist
@@ -57,15 +64,20 @@ def _rank_main(rank, port, kw, seed, out_dir):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("kw,seed", [
-    (dict(), 3),
-    (dict(samplesPerIteration=4096, batchRule="fill", maxTreeSize=200000, numIterations=15, goalThreshold=0.0), 21),
-    (dict(fixGNewClear=True, numIterations=40), 8),
+@pytest.mark.parametrize("kw,seed,exchange", [
+    (dict(), 3, "oneshot"),
+    (dict(samplesPerIteration=4096, batchRule="fill", maxTreeSize=200000, numIterations=15, goalThreshold=0.0), 21,
+     "oneshot"),
+    (dict(fixGNewClear=True, numIterations=40), 8, "oneshot"),
+    (dict(), 3, "collective"),
+    (dict(samplesPerIteration=4096, batchRule="fill", maxTreeSize=200000, numIterations=15, goalThreshold=0.0), 21,
+     "collective"),
 ])
-def test_two_processes_one_gpu_bit_exact(kw, seed, tmp_path, obstacles, oracle_lib):
+def test_two_processes_one_gpu_bit_exact(kw, seed, exchange, tmp_path, obstacles, oracle_lib):
     ctx = mp.get_context("spawn")
     port = _free_port()
-    procs = [ctx.Process(target=_rank_main, args=(r, port, kw, seed, str(tmp_path))) for r in range(WORLD)]
+    procs = [ctx.Process(target=_rank_main, args=(r, port, kw, seed, str(tmp_path), exchange))
+             for r in range(WORLD)]
     for pr in procs:
         pr.start()
     for pr in procs:
