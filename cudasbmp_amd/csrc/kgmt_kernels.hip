@@ -684,7 +684,7 @@ __device__ __forceinline__ void store_record(float4* p, float4 v) {
                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-__global__ __launch_bounds__(kBlock) void k_pack(KgmtDev d, int t) {
+__device__ __forceinline__ void pack_block(const KgmtDev& d, int t) {
     __shared__ int sRed[3][kBlock / kWave];
     __shared__ int sWaveCnt[kBlock / kWave];
     const int lane = threadIdx.x & (kWave - 1);
@@ -718,9 +718,14 @@ __global__ __launch_bounds__(kBlock) void k_pack(KgmtDev d, int t) {
     const int next = gblock + d.nranks;   // H never decreases: blocks >= H never ran, entries past them are unused
     const bool last = (long long)next * kBlock >= c.H;
     const int hi = last ? d.nBlocks : min(next, d.nBlocks);
-    for (int g = gblock + 1 + (int)threadIdx.x; g <= hi; g += kBlock) d.pfxOut[g] = preLocal + cnt;
-    if (last && threadIdx.x == 0) d.totOut[d.rank] = preLocal + cnt;
+    // written through (device scope): k_pack_x's exchange workgroups read them in this launch
+    for (int g = gblock + 1 + (int)threadIdx.x; g <= hi; g += kBlock)
+        __hip_atomic_store(d.pfxOut + g, preLocal + cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (last && threadIdx.x == 0)
+        __hip_atomic_store(d.totOut + d.rank, preLocal + cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+
+__global__ __launch_bounds__(kBlock) void k_pack(KgmtDev d, int t) { pack_block(d, t); }
 
 // Local shard group (P ranks on one device, one stream): the all-reduce of the
 // exchange buffers as a sum kernel.
@@ -775,16 +780,21 @@ constexpr int kOneshotChunks = 8;
 struct OneshotArgs {
     unsigned long long* inbox[kMaxRanks];
 };
-__global__ __launch_bounds__(kBlock) void k_oneshot(OneshotArgs a, const unsigned long long* __restrict__ send,
-                                                    unsigned long long* __restrict__ recv, long long n, int nranks,
-                                                    int rank, unsigned long long seq, int* error) {
-    const int c = blockIdx.x;
+// Chunk c of the exchange.  coherentSend: `send` was written by other workgroups of
+// this launch (k_pack's fused form), so it is read with device-scope loads.
+template <bool kCoherentSend>
+__device__ __forceinline__ void oneshot_chunk(const OneshotArgs& a, const unsigned long long* __restrict__ send,
+                                              unsigned long long* __restrict__ recv, long long n, int nranks,
+                                              int rank, unsigned long long seq, int* error, int c) {
     const long long per = (n + kOneshotChunks - 1) / kOneshotChunks;
     const long long lo = c * per, hi = min(n, lo + per);
     const size_t par = (size_t)(seq & 1ull) * nranks * n;
     const size_t flags = (size_t)2 * nranks * n;
     for (long long i = lo + threadIdx.x; i < hi; i += kBlock) {
-        const unsigned long long v = send[i];
+        const unsigned long long v =
+            kCoherentSend ? __hip_atomic_load(const_cast<unsigned long long*>(send) + i, __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_AGENT)
+                          : send[i];
         for (int q = 0; q < nranks; ++q)
             __hip_atomic_store(a.inbox[q] + par + (size_t)rank * n + i, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
@@ -813,6 +823,56 @@ __global__ __launch_bounds__(kBlock) void k_oneshot(OneshotArgs a, const unsigne
                                      __HIP_MEMORY_SCOPE_SYSTEM);
         recv[i] = sum;
     }
+}
+
+__global__ __launch_bounds__(kBlock) void k_oneshot(OneshotArgs a, const unsigned long long* __restrict__ send,
+                                                    unsigned long long* __restrict__ recv, long long n, int nranks,
+                                                    int rank, unsigned long long seq, int* error) {
+    oneshot_chunk<false>(a, send, recv, n, nranks, rank, seq, error, (int)blockIdx.x);
+}
+
+// k_pack and the one-shot exchange in one launch: workgroups 0..nPack-1 pack (each
+// sets its flag arrive[b] = seq once its stores are visible device-wide), the last
+// kOneshotChunks workgroups -- dispatched after every packer -- wait until every
+// packer's flag reads seq, then exchange as k_oneshot does.  Saves a dependent launch
+// per iteration.
+struct PackXArgs {
+    OneshotArgs a;
+    const unsigned long long* send;   // this rank's exchange buffer (deltas first: d.deltaOut)
+    unsigned long long* recv;
+    long long n;
+    unsigned long long seq;
+    unsigned long long* arrive;   // [nPack] packer flags, monotone (seq)
+    int nPack;
+};
+__global__ __launch_bounds__(kBlock) void k_pack_x(KgmtDev d, int t, PackXArgs x) {
+    if ((int)blockIdx.x >= x.nPack) {
+        // every packer's flag: one word each (1,024 same-address device atomics would
+        // serialise at the memory side: 131 us per launch, measured)
+        const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
+        for (;;) {
+            bool ok = true;
+            for (int b = threadIdx.x; b < x.nPack; b += kBlock)
+                ok &= __hip_atomic_load(x.arrive + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= x.seq;
+            if (__syncthreads_and(ok)) break;
+            if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > 100000000ll) {   // uniform enough: all
+                if (threadIdx.x == 0) atomicExch(&d.status->error, 1);            // threads passed the barrier
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+        oneshot_chunk<true>(x.a, x.send, x.recv, x.n, d.nranks, d.rank, x.seq, &d.status->error,
+                            (int)blockIdx.x - x.nPack);
+        return;
+    }
+    pack_block(d, t);
+    // Its exchange-buffer and record stores are written through: once every wave's
+    // have completed, the flag may follow.  (__threadfence() would write back the whole
+    // L2 of the XCD, per packer: 127 us per launch, measured.)
+    __builtin_amdgcn_s_waitcnt(0);
+    __syncthreads();
+    if (threadIdx.x == 0)
+        __hip_atomic_store(x.arrive + blockIdx.x, x.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 size_t oneshot_inbox_words(long long n, int nranks) { return (size_t)2 * nranks * n + (size_t)nranks * kOneshotChunks; }
@@ -1650,6 +1710,20 @@ void launch_oneshot(unsigned long long* const* inbox, const unsigned long long* 
 
 void launch_finish(const KgmtDev& d, int t, int insertBlocks, hipStream_t s, const KernelTiming& tm) {
     launch(k_finish, dim3(1 + insertBlocks), dim3(kBlock), 0, s, tm, d, t);
+}
+
+void launch_pack_exchange(const KgmtDev& d, int t, int blocks, unsigned long long* const* inbox,
+                          const unsigned long long* send, unsigned long long* recv, long long n,
+                          unsigned long long seq, unsigned long long* arrive, hipStream_t s, const KernelTiming& tm) {
+    PackXArgs x{};
+    for (int q = 0; q < d.nranks; ++q) x.a.inbox[q] = inbox[q];
+    x.send = send;
+    x.recv = recv;
+    x.n = n;
+    x.seq = seq;
+    x.arrive = arrive;
+    x.nPack = blocks;
+    launch(k_pack_x, dim3(blocks + kOneshotChunks), dim3(kBlock), 0, s, tm, d, t, x);
 }
 
 void launch_pack(const KgmtDev& d, int t, int blocks, hipStream_t s, const KernelTiming& tm) {

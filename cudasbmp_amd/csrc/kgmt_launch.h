@@ -39,6 +39,12 @@ size_t oneshot_inbox_words(long long n, int nranks);
 void launch_oneshot(unsigned long long* const* inbox, const unsigned long long* send, unsigned long long* recv,
                     long long n, int nranks, int rank, unsigned long long seq, int* error, hipStream_t s,
                     const KernelTiming& tm = KernelTiming());
+// k_pack and that exchange in one launch (blocks packers + the exchange workgroups);
+// arrive: blocks zeroed u64 packer flags kept for the planner's lifetime.
+void launch_pack_exchange(const KgmtDev& d, int t, int blocks, unsigned long long* const* inbox,
+                          const unsigned long long* send, unsigned long long* recv, long long n,
+                          unsigned long long seq, unsigned long long* arrive, hipStream_t s,
+                          const KernelTiming& tm = KernelTiming());
 // Local shard group: recv[q][i] = sum over ranks of send[r][i], for every rank q.
 void launch_xsum(const unsigned long long* const* send, unsigned long long* const* recv, int nranks, long long n,
                  hipStream_t s);

@@ -278,6 +278,13 @@ KgmtPlanner::KgmtPlanner(const sbmp_kgmt_params& p, int nranks, int rank, Exchan
             ex_->share_buffer(own, sizeof(unsigned long long) * words, ib);
             for (int q = 0; q < nranks; ++q) inbox_[q] = static_cast<unsigned long long*>(ib[q]);
             oneshot_ = true;
+            arrive_ = alloc<unsigned long long>(expandBlocks_);
+            SBMP_HIP(hipMemset(arrive_, 0, sizeof(unsigned long long) * expandBlocks_));
+            SBMP_HIP(hipDeviceSynchronize());
+            // SBMP_EXCHANGE=fused: the exchange inside k_pack's launch (k_pack_x).  Two
+            // ranks sharing one GPU measured 12.2 vs 12.9 G samples/s for the separate
+            // launch, so the separate launch is the default.
+            fusedPack_ = v && std::string(v) == "fused";
         }
     }
 }
@@ -431,10 +438,18 @@ void KgmtPlanner::stage_expand(int t) {
     launch_expand(d_, t, p_.agent, expandBlocks_, expandVariant_, stream_, timing(K_EXPAND));
 }
 
-void KgmtPlanner::stage_pack(int t) { launch_pack(d_, t, expandBlocks_, stream_, timing(K_PACK)); }
+void KgmtPlanner::stage_pack(int t) {
+    if (oneshot_ && fusedPack_) {   // k_pack + the exchange in one launch (stage_exchange then does nothing)
+        ++xSeq_;
+        launch_pack_exchange(d_, t, expandBlocks_, inbox_, xSend_, xRecv_, (long long)xWords_, xSeq_, arrive_,
+                             stream_, timing(K_PACK));
+        return;
+    }
+    launch_pack(d_, t, expandBlocks_, stream_, timing(K_PACK));
+}
 
 void KgmtPlanner::stage_exchange() {
-    if (!ex_) return;
+    if (!ex_ || (oneshot_ && fusedPack_)) return;
     if (oneshot_) {
         ++xSeq_;
         launch_oneshot(inbox_, xSend_, xRecv_, (long long)xWords_, d_.nranks, d_.rank, xSeq_, &d_.status->error,
