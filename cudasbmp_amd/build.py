@@ -37,6 +37,8 @@ COMMON = [
     "-I", os.path.join(ROOT, "include"), "-I", CSRC,
     "-Wall", "-Wno-unused-result",
 ]
+# Extra compile flags for experiments (e.g. scheduler strategies in an A/B variant).
+EXTRA = os.environ.get("SBMP_HIPCC_FLAGS", "").split()
 LINK = ["-shared", f"--offload-arch={ARCH}", "-L/opt/rocm/lib", "-lrccl", "-Wl,-rpath,/opt/rocm/lib"]
 
 
@@ -54,7 +56,7 @@ def _compile(src: str, force: bool, verbose: bool) -> str:
     if not force and os.path.exists(obj) and os.path.getmtime(obj) >= newest_dep:
         return obj
     lang = ["-x", "hip"] if src.endswith(".hip") else []
-    cmd = [HIPCC] + COMMON + lang + ["-c", src, "-o", obj]
+    cmd = [HIPCC] + COMMON + EXTRA + lang + ["-c", src, "-o", obj]
     if verbose:
         print(" ".join(cmd), flush=True)
     r = subprocess.run(cmd, capture_output=True, text=True)

@@ -9,5 +9,5 @@ defs=""
 for m in "$@"; do defs="$defs#define $m\n"; done
 f=_ab/$name/cudasbmp_amd/csrc/kgmt_kernels.hip
 printf "$defs" | sed 's/=/ /' | cat - $f > $f.new && mv $f.new $f
-(cd _ab/$name && python3 -m cudasbmp_amd.build --force > /dev/null)
+(cd _ab/$name && python3 -m cudasbmp_amd.build --force > /dev/null) || { echo "build failed"; exit 1; }
 echo "built _ab/$name with: $*"
