@@ -38,6 +38,9 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("dir")
     ap.add_argument("--skip", type=int, default=25)
+    ap.add_argument("--stat", choices=("median", "mean"), default="median",
+                    help="mean: for runs whose launches differ in size (c5), so that counts per child "
+                         "match the bench's mean S over the same launches")
     ap.add_argument("--json", default=None)
     ap.add_argument("--samples-per-launch", type=float, default=None,
                     help="children per k_expand / k_step launch in the profiled run (for bytes/child)")
@@ -48,7 +51,8 @@ def main():
             short = kern.split("(")[0].replace("void ", "").replace("sbmp::", "")
             for c, vals in ctrs.items():
                 v = np.array(vals[a.skip:] if len(vals) > a.skip + 3 else vals)
-                summary.setdefault(short, {})[c] = float(np.median(v))
+                summary.setdefault(short, {})[c] = float(np.median(v) if a.stat == "median" else np.mean(v))
+                summary[short]["dispatches"] = float(len(v))
     for k, cs in summary.items():
         print(k)
         for c, v in sorted(cs.items()):
@@ -57,6 +61,7 @@ def main():
         out = {}
         for k, cs in summary.items():
             if "FETCH_SIZE" in cs and "WRITE_SIZE" in cs:
+                cs.pop("dispatches", None)
                 rd = 2.0 * cs["FETCH_SIZE"] * 1024.0
                 wr = cs["WRITE_SIZE"] * 1024.0
                 key = "k_expand" if k.startswith("k_expand") else "k_step" if k.startswith("k_step") else k
