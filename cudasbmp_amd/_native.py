@@ -104,7 +104,7 @@ EXPORTED_SYMBOLS = (
     "sbmp_kgmt_create_sharded_host", "sbmp_expand_batch", "sbmp_expand_batch_host", "sbmp_insert_batch",
     "sbmp_device_alloc", "sbmp_device_copy_to", "sbmp_device_copy_from", "sbmp_kgmt_set_iteration_dump",
     "sbmp_load_system_config",
-    "sbmp_obstacle_grid_query", "sbmp_kgmt_solution_path", "sbmp_random_tree",
+    "sbmp_obstacle_grid_query", "sbmp_kgmt_solution_path", "sbmp_random_tree", "sbmp_hbm_copy_bandwidth",
 )
 
 _lib = None
@@ -172,6 +172,7 @@ def lib():
         "sbmp_device_upload_f32": [vp, ctypes.c_size_t, P(vp)],
         "sbmp_device_free": [vp],
         "sbmp_device_count": [P(i)],
+        "sbmp_hbm_copy_bandwidth": [ctypes.c_size_t, i, P(ctypes.c_double)],
     }
     for name, args in sig.items():
         f = getattr(L, name)

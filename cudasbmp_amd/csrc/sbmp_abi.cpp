@@ -27,6 +27,7 @@ void comm_get_unique_id(uint8_t* id);
 void expand_batch(const sbmp_expand_batch_args* args, void* stream);   // batch.hip
 void expand_batch_host(const sbmp_expand_batch_args* args);
 void insert_batch(const sbmp_insert_batch_args* args, void* stream);
+double hbm_copy_bandwidth(size_t bytes, int reps);
 void load_system_config(const char* path, sbmp_system_config* out);   // config.cpp
 }  // namespace sbmp
 
@@ -515,6 +516,14 @@ sbmp_status sbmp_device_count(int* count) {
         int n = 0;
         hipError_t e = hipGetDeviceCount(&n);
         *count = (e == hipSuccess) ? n : 0;
+    });
+}
+
+sbmp_status sbmp_hbm_copy_bandwidth(size_t bytes, int reps, double* gbs) {
+    return guarded([&] {
+        REQUIRE(gbs, "NULL output");
+        *gbs = 0.0;
+        *gbs = sbmp::hbm_copy_bandwidth(bytes, reps);
     });
 }
 

@@ -103,6 +103,13 @@ def device_count() -> int:
     return n.value
 
 
+def hbm_copy_bandwidth(nbytes: int = 4 << 30, reps: int = 5) -> float:
+    """Measured HBM copy bandwidth of the current device in GB/s (sbmp_hbm_copy_bandwidth)."""
+    g = ctypes.c_double()
+    nat.call("sbmp_hbm_copy_bandwidth", ctypes.c_size_t(nbytes), reps, ctypes.byref(g))
+    return g.value
+
+
 def _vec7(v) -> np.ndarray:
     a = np.zeros(7, dtype=np.float32)
     v = np.asarray(v, dtype=np.float32).ravel()

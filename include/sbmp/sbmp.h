@@ -288,6 +288,10 @@ sbmp_status sbmp_device_alloc(size_t bytes, void** d_out);
 sbmp_status sbmp_device_copy_to(void* d_dst, const void* host, size_t bytes);
 sbmp_status sbmp_device_copy_from(void* host, const void* d_src, size_t bytes);
 sbmp_status sbmp_device_count(int* count);
+/* Measured HBM copy bandwidth of the current device (the STREAM-copy
+ * figure quoted next to the 8 TB/s spec): a 16-B-per-lane copy of `bytes` (>= 1 MiB)
+ * into a second buffer, best of `reps` passes, GB/s = 2 x bytes / time. */
+sbmp_status sbmp_hbm_copy_bandwidth(size_t bytes, int reps, double* gbs);
 
 /* ---- Multi-GPU: one planning problem sharded over ranks (one process per GPU) ----
  * Slots are owned block-cyclically (slot s -> rank (s/256) mod nranks); every
