@@ -132,6 +132,11 @@ struct KgmtDev {
     int recCap;
     float4* recOut;
     const float4* recPeer[kMaxRanks];
+    // Sharded ranks with the pack folded into k_expand (packInExpand): per owned block,
+    // t << 33 | inclusive << 32 | count, published for the next blocks' look-back
+    // (DESIGN.md §7); zeroed by begin(), so tags of an earlier plan never match.
+    unsigned long long* packLook;
+    int packInExpand;
     // Region tables: R1, R1Avail, R1Valid, R1Invalid, R1Cov are the parity-0 slices
     // of one int array [2][5][nR1], R2Avail of [2][nR2/32].  k_finish updates parity
     // 0 in place; k_step (below) reads iteration t-1's parity and writes t's.

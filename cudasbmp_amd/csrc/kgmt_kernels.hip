@@ -97,6 +97,76 @@ __device__ __forceinline__ float4 load_record(const float4* p) {
 }
 
 // ------------------------------------------------------------------ expand
+// A sharded record word pair, stored through to memory (peers read it over xGMI).
+__device__ __forceinline__ void store_record(float4* p, float4 v) {
+    unsigned long long* q = reinterpret_cast<unsigned long long*>(p);
+    __hip_atomic_store(q, ((unsigned long long)__float_as_uint(v.y) << 32) | __float_as_uint(v.x), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(q + 1, ((unsigned long long)__float_as_uint(v.w) << 32) | __float_as_uint(v.z),
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// Sharded ranks, k_pack folded into k_expand: the block's offset among
+// this rank's owned blocks is the sum of the earlier blocks' counts, which each block
+// publishes as t << 32 | count (one untorn 8-B store, self-validating by its tag);
+// the whole workgroup reads the earlier entries at once and re-reads until every tag
+// is t (earlier blocks were dispatched first and never wait on later ones).  Then the
+// records, the exchange's prefix fields and the rank total, as pack_block writes them.
+__device__ __forceinline__ void expand_pack(const KgmtDev& d, int t, const IterCtrl& c, int gblock, int cnt,
+                                            bool flagged, int idx, float4 cs, float4 cc) {
+    __shared__ int sPart[kBlock / kWave];
+    const int lb = (int)blockIdx.x;
+    const unsigned want = (unsigned)t;
+    unsigned long long* const look = d.packLook;
+    if (threadIdx.x == 0)
+        __hip_atomic_store(look + lb, (unsigned long long)want << 32 | (unsigned)cnt, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    int part = 0;
+    if (lb > 0) {
+        const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
+        // Blocks finish roughly in dispatch order: one lane first waits for the block
+        // just before (one line), so the full read below mostly succeeds at once
+        // instead of every workgroup re-reading all earlier entries.
+        if (threadIdx.x == 0) {
+            while ((unsigned)(__hip_atomic_load(look + lb - 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >> 32) != want &&
+                   (long long)__builtin_amdgcn_s_memrealtime() - t0 <= 100000000ll)
+                __builtin_amdgcn_s_sleep(1);
+        }
+        __syncthreads();
+        for (;;) {
+            bool ok = true;
+            part = 0;
+            for (int i = (int)threadIdx.x; i < lb; i += kBlock) {
+                const unsigned long long v = __hip_atomic_load(look + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                ok &= (unsigned)(v >> 32) == want;
+                part += (int)(uint32_t)v;
+            }
+            if (__syncthreads_and(ok)) break;
+            // 1 s: report, do not hang (decided by a barrier, so every wave leaves together)
+            if (__syncthreads_or((long long)__builtin_amdgcn_s_memrealtime() - t0 > 100000000ll)) {
+                if (threadIdx.x == 0) atomicExch(&d.status->error, 1);
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+    }
+    part = wave_sum(part);
+    if ((threadIdx.x & (kWave - 1)) == 0) sPart[threadIdx.x >> 6] = part;
+    __syncthreads();
+    const int preLocal = sPart[0] + sPart[1] + sPart[2] + sPart[3];
+    if (flagged) {
+        float4* rec = d.recOut + ((size_t)(t & 1) * d.recCap + preLocal + idx) * kRecordF4;
+        store_record(rec, cs);
+        store_record(rec + 1, cc);
+        store_record(rec + 2, make_float4(__int_as_float(gblock), __int_as_float(idx), 0.0f, 0.0f));
+    }
+    const int next = gblock + d.nranks;   // H never decreases: blocks >= H never ran, entries past them are unused
+    const bool last = (long long)next * kBlock >= c.H;
+    const int hi = last ? d.nBlocks : min(next, d.nBlocks);
+    for (int g = gblock + 1 + (int)threadIdx.x; g <= hi; g += kBlock) d.pfxOut[g] = preLocal + cnt;
+    if (last && threadIdx.x == 0) d.totOut[d.rank] = preLocal + cnt;
+}
+
 // One thread per child slot, 256-slot workgroups.  Outputs: child state/controls/
 // parent (2 x 16 B), XORWOW state (16 + 8 B), GNew bits (one 8-B word per wave),
 // the GNew popcount of the workgroup, and the region bookkeeping of
@@ -188,6 +258,7 @@ __global__ __launch_bounds__(kBlock) void k_expand(KgmtDev d, int t) {
     const float4* obs = (kRegObs > 0) ? ro : kLdsObs ? sObs : d.obstacles;
 
     bool accept = false;
+    float4 cs = make_float4(0.f, 0.f, 0.f, 0.f), cc = cs;   // this slot's child (state, ctrl): the packed record
     if (act) {
         Xorwow rs{ra.x, ra.y, ra.z, ra.w, rb.x, rb.y};
         ChildOut out;
@@ -205,8 +276,10 @@ __global__ __launch_bounds__(kBlock) void k_expand(KgmtDev d, int t) {
                 if (!r2Avail) atomicOr(&sNew[r2 >> 5], bit);
             }
         }
-        store_wt(d.uState, slot, out.state);   // write-through: fewer dirty lines at the boundary
-        store_wt(d.uCtrl, slot, make_float4(out.a, out.steer, out.dur, __int_as_float(parent)));
+        cs = out.state;
+        cc = make_float4(out.a, out.steer, out.dur, __int_as_float(parent));
+        store_wt(d.uState, slot, cs);   // write-through: fewer dirty lines at the boundary
+        store_wt(d.uCtrl, slot, cc);
         store_wt(d.rngA, slot, make_uint4(rs.v0, rs.v1, rs.v2, rs.v3));
         store_wt(d.rngB, slot, make_uint2(rs.v4, rs.d));
         if (r1 >= 0) atomicAdd(&sR1P[r1], valid ? 1 : 0x10000);
@@ -221,15 +294,28 @@ __global__ __launch_bounds__(kBlock) void k_expand(KgmtDev d, int t) {
     // GNew |= accept (stale bits survive, D6).  A wave covers one 64-bit word; it is
     // always written (a sharded rank's Out word must carry its stale bits too).
     const unsigned long long mask = __ballot(accept);
+    const unsigned long long now =   // this wave's GNew word, in every lane
+        ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)(oldWord >> 32), 0) << 32 |
+         (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)oldWord, 0)) | mask;
     if (lane == 0) {
-        const unsigned long long now = oldWord | mask;
         d.gnewOut[slot >> 6] = now;
         sWaveCnt[wave] = __popcll(now);   // slots past S: the stale bits' count
     }
     SBMP_STAMP(4);
     __syncthreads();
     SBMP_STAMP(5);
-    if (tid == 0) d.blockCountOut[gblock] = sWaveCnt[0] + sWaveCnt[1] + sWaveCnt[2] + sWaveCnt[3];
+    const int cntB = sWaveCnt[0] + sWaveCnt[1] + sWaveCnt[2] + sWaveCnt[3];
+    if (tid == 0) d.blockCountOut[gblock] = cntB;
+    if (d.packInExpand) {   // sharded rank: k_pack's work, without its launch
+        int inBlock = 0;
+        for (int i = 0; i < wave; ++i) inBlock += sWaveCnt[i];
+        const bool flagged = (now >> lane) & 1ull;
+        if (__ballot(flagged && !act) != 0ull && flagged && !act) {   // a stale flag past S: the slot's last child
+            cs = d.uState[slot];
+            cc = d.uCtrl[slot];
+        }
+        expand_pack(d, t, c, gblock, cntB, flagged, inBlock + __popcll(now & ((1ull << lane) - 1ull)), cs, cc);
+    }
     {   // one 64-bit atomic per touched cell, into this workgroup's replica
         unsigned long long* const rep = d.deltaOut + (size_t)(blockIdx.x % kDeltaReps) * d.nR1;
         const int v = sR1P[tid];   // nR1 == kBlock
@@ -676,13 +762,6 @@ __device__ void owner_clear(const KgmtDev& d, int t, int lb) {
 // its owner-local offset, and this rank's share of the global prefix of every block
 // up to its next owned block (the last active block: up to the total), so the
 // all-reduce's sum hands every insert block its offset and the total in O(1).
-__device__ __forceinline__ void store_record(float4* p, float4 v) {
-    unsigned long long* q = reinterpret_cast<unsigned long long*>(p);
-    __hip_atomic_store(q, ((unsigned long long)__float_as_uint(v.y) << 32) | __float_as_uint(v.x), __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_SYSTEM);
-    __hip_atomic_store(q + 1, ((unsigned long long)__float_as_uint(v.w) << 32) | __float_as_uint(v.z),
-                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-}
 
 __device__ __forceinline__ void pack_block(const KgmtDev& d, int t) {
     __shared__ int sRed[3][kBlock / kWave];

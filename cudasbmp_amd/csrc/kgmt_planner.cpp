@@ -242,6 +242,8 @@ KgmtPlanner::KgmtPlanner(const sbmp_kgmt_params& p, int nranks, int rank, Exchan
     d.recOut = d.sharded ? alloc<float4>((size_t)2 * kRecordF4 * d.recCap) : nullptr;
     for (int q = 0; q < kMaxRanks; ++q) d.recPeer[q] = nullptr;
     d.recPeer[rank] = d.recOut;
+    d.packLook = d.sharded ? alloc<unsigned long long>(expandBlocks_) : nullptr;
+    d.packInExpand = 0;   // set below, once the exchange is chosen
     d.logSlots = expandBlocks_ * kBlock;
     d.r2log = (d.nR2 <= kLogMaxR2) ? alloc<uint16_t>((size_t)kFoldEvery * d.logSlots) : nullptr;
     d.ctrl = alloc<IterCtrl>(p.numIterations + 2);
@@ -287,6 +289,14 @@ KgmtPlanner::KgmtPlanner(const sbmp_kgmt_params& p, int nranks, int rank, Exchan
             fusedPack_ = v && std::string(v) == "fused";
         }
     }
+    // SBMP_PACK=expand: sharded ranks pack their records inside k_expand (each block
+    // sums the earlier owned blocks' published counts) instead of a k_pack launch.  A
+    // local group of 8 measured k_expand 16.6 us vs 13.3 + 4.5 us for k_expand + k_pack,
+    // one launch fewer; two ranks sharing one GPU measured 11.7 vs 12.6 G samples/s
+    // (DESIGN.md §7), so the separate launch stays the default.  k_pack_x
+    // (SBMP_EXCHANGE=fused) needs the separate pack.
+    const char* pk = getenv("SBMP_PACK");
+    d.packInExpand = (d.sharded && !fusedPack_ && pk && std::string(pk) == "expand") ? 1 : 0;
 }
 
 KgmtPlanner::~KgmtPlanner() {
@@ -333,6 +343,7 @@ void KgmtPlanner::begin(const float* initial, const float* goal, const float* d_
         SBMP_HIP(hipMemsetAsync(d.stepR2New, 0, sizeof(uint32_t) * 3 * (d.nR2 / 32), s));
     }
     SBMP_HIP(hipMemsetAsync(d.R2Snap, 0, sizeof(uint32_t) * (d.nR2 / 32), s));
+    if (d.packLook) SBMP_HIP(hipMemsetAsync(d.packLook, 0, sizeof(unsigned long long) * expandBlocks_, s));
     SBMP_HIP(hipMemsetAsync(d.R2Valid, 0, sizeof(int) * d.nR2, s));
     SBMP_HIP(hipMemsetAsync(d.R2Invalid, 0, sizeof(int) * d.nR2, s));
     launch_fill_f32(d.R1Score, 1.0f, 2 * d.nR1, s);
@@ -439,6 +450,7 @@ void KgmtPlanner::stage_expand(int t) {
 }
 
 void KgmtPlanner::stage_pack(int t) {
+    if (d_.packInExpand) return;   // k_expand packed already
     if (oneshot_ && fusedPack_) {   // k_pack + the exchange in one launch (stage_exchange then does nothing)
         ++xSeq_;
         launch_pack_exchange(d_, t, expandBlocks_, inbox_, xSend_, xRecv_, (long long)xWords_, xSeq_, arrive_,
