@@ -181,7 +181,7 @@ __device__ __forceinline__ void expand_pack(const KgmtDev& d, int t, const IterC
 //               scattered device atomics run ~17x below the contiguous rate
 //               (MI355X_MICROARCH.md, global atomics); nothing reads these two
 //               arrays during the run (KGMT.cu:405,410 are write-only).
-template <int AGENT, int OBS>
+template <int AGENT, int OBS, bool PACK = false>
 __global__ __launch_bounds__(kBlock) void k_expand(KgmtDev d, int t) {
     extern __shared__ float4 sObs[];
     __shared__ float sScore[kMaxR1];
@@ -294,10 +294,8 @@ __global__ __launch_bounds__(kBlock) void k_expand(KgmtDev d, int t) {
     // GNew |= accept (stale bits survive, D6).  A wave covers one 64-bit word; it is
     // always written (a sharded rank's Out word must carry its stale bits too).
     const unsigned long long mask = __ballot(accept);
-    const unsigned long long now =   // this wave's GNew word, in every lane
-        ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)(oldWord >> 32), 0) << 32 |
-         (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)oldWord, 0)) | mask;
     if (lane == 0) {
+        const unsigned long long now = oldWord | mask;
         d.gnewOut[slot >> 6] = now;
         sWaveCnt[wave] = __popcll(now);   // slots past S: the stale bits' count
     }
@@ -306,15 +304,24 @@ __global__ __launch_bounds__(kBlock) void k_expand(KgmtDev d, int t) {
     SBMP_STAMP(5);
     const int cntB = sWaveCnt[0] + sWaveCnt[1] + sWaveCnt[2] + sWaveCnt[3];
     if (tid == 0) d.blockCountOut[gblock] = cntB;
-    if (d.packInExpand) {   // sharded rank: k_pack's work, without its launch
-        int inBlock = 0;
-        for (int i = 0; i < wave; ++i) inBlock += sWaveCnt[i];
-        const bool flagged = (now >> lane) & 1ull;
-        if (__ballot(flagged && !act) != 0ull && flagged && !act) {   // a stale flag past S: the slot's last child
-            cs = d.uState[slot];
-            cc = d.uCtrl[slot];
+    // Sharded rank with SBMP_PACK=expand: k_pack's work without its launch, in separate
+    // instantiations of the register obstacle forms (the host packs with k_pack
+    // otherwise): compiled into every form, the extra live state cost c5 3% (63.97 vs
+    // 61.9 us per k_expand at 1M children) and the register forms an occupancy step.
+    if constexpr (PACK) {
+        {
+            const unsigned long long now =   // this wave's GNew word, in every lane
+                ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)(oldWord >> 32), 0) << 32 |
+                 (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)oldWord, 0)) | mask;
+            int inBlock = 0;
+            for (int i = 0; i < wave; ++i) inBlock += sWaveCnt[i];
+            const bool flagged = (now >> lane) & 1ull;
+            if (__ballot(flagged && !act) != 0ull && flagged && !act) {   // a stale flag past S: the slot's last child
+                cs = d.uState[slot];
+                cc = d.uCtrl[slot];
+            }
+            expand_pack(d, t, c, gblock, cntB, flagged, inBlock + __popcll(now & ((1ull << lane) - 1ull)), cs, cc);
         }
-        expand_pack(d, t, c, gblock, cntB, flagged, inBlock + __popcll(now & ((1ull << lane) - 1ull)), cs, cc);
     }
     {   // one 64-bit atomic per touched cell, into this workgroup's replica
         unsigned long long* const rep = d.deltaOut + (size_t)(blockIdx.x % kDeltaReps) * d.nR1;
@@ -1700,6 +1707,21 @@ static void launch(K kernel, dim3 grid, dim3 block, size_t shm, hipStream_t s, c
         hipLaunchKernelGGL(kernel, grid, block, shm, s, args...);
 }
 
+template <int AGENT, bool PACK>
+static void launch_expand_reg(const KgmtDev& d, int t, dim3 grid, dim3 block, hipStream_t s, const KernelTiming& tm) {
+    switch (d.nObs) {   // the box count is a compile-time constant of the register path
+        case 0: launch(k_expand<AGENT, kObsReg + 0, PACK>, grid, block, 0, s, tm, d, t); break;
+        case 1: launch(k_expand<AGENT, kObsReg + 1, PACK>, grid, block, 0, s, tm, d, t); break;
+        case 2: launch(k_expand<AGENT, kObsReg + 2, PACK>, grid, block, 0, s, tm, d, t); break;
+        case 3: launch(k_expand<AGENT, kObsReg + 3, PACK>, grid, block, 0, s, tm, d, t); break;
+        case 4: launch(k_expand<AGENT, kObsReg + 4, PACK>, grid, block, 0, s, tm, d, t); break;
+        case 5: launch(k_expand<AGENT, kObsReg + 5, PACK>, grid, block, 0, s, tm, d, t); break;
+        case 6: launch(k_expand<AGENT, kObsReg + 6, PACK>, grid, block, 0, s, tm, d, t); break;
+        case 7: launch(k_expand<AGENT, kObsReg + 7, PACK>, grid, block, 0, s, tm, d, t); break;
+        default: launch(k_expand<AGENT, kObsReg + 8, PACK>, grid, block, 0, s, tm, d, t); break;
+    }
+}
+
 template <int AGENT>
 static void launch_expand_agent(const KgmtDev& d, int t, int blocks, int variant, hipStream_t s,
                                 const KernelTiming& tm) {
@@ -1710,22 +1732,19 @@ static void launch_expand_agent(const KgmtDev& d, int t, int blocks, int variant
     } else if (d.nObs > kMaxLdsObs) {
         launch(k_expand<AGENT, kObsGlobal>, grid, block, 0, s, tm, d, t);
     } else if (d.nObs <= kMaxRegObs && (variant == 0 || variant == 3)) {
-        switch (d.nObs) {   // the box count is a compile-time constant of the register path
-            case 0: launch(k_expand<AGENT, kObsReg + 0>, grid, block, 0, s, tm, d, t); break;
-            case 1: launch(k_expand<AGENT, kObsReg + 1>, grid, block, 0, s, tm, d, t); break;
-            case 2: launch(k_expand<AGENT, kObsReg + 2>, grid, block, 0, s, tm, d, t); break;
-            case 3: launch(k_expand<AGENT, kObsReg + 3>, grid, block, 0, s, tm, d, t); break;
-            case 4: launch(k_expand<AGENT, kObsReg + 4>, grid, block, 0, s, tm, d, t); break;
-            case 5: launch(k_expand<AGENT, kObsReg + 5>, grid, block, 0, s, tm, d, t); break;
-            case 6: launch(k_expand<AGENT, kObsReg + 6>, grid, block, 0, s, tm, d, t); break;
-            case 7: launch(k_expand<AGENT, kObsReg + 7>, grid, block, 0, s, tm, d, t); break;
-            default: launch(k_expand<AGENT, kObsReg + 8>, grid, block, 0, s, tm, d, t); break;
-        }
+        if (d.packInExpand) launch_expand_reg<AGENT, true>(d, t, grid, block, s, tm);
+        else launch_expand_reg<AGENT, false>(d, t, grid, block, s, tm);
     } else if (variant == 2) {
         launch(k_expand<AGENT, kObsLds4>, grid, block, shm, s, tm, d, t);
     } else {
         launch(k_expand<AGENT, kObsLds>, grid, block, shm, s, tm, d, t);
     }
+}
+
+// k_expand packs the sharded records itself (SBMP_PACK=expand) only in its register
+// obstacle forms; launch_expand_agent picks one of those exactly in this case.
+bool expand_packs_records(const KgmtDev& d, int variant) {
+    return !d.gridStart && d.nObs <= kMaxLdsObs && d.nObs <= kMaxRegObs && (variant == 0 || variant == 3);
 }
 
 void launch_expand(const KgmtDev& d, int t, int agent, int blocks, int variant, hipStream_t s,

@@ -19,6 +19,7 @@ struct KernelTiming {
 // variant: obstacle form: 0 = auto, 1 = LDS rolled, 2 = LDS 4-way batched, 3 = registers
 // (lists of at most kMaxRegObs boxes; auto picks it there, else 1); lists longer
 // than kMaxLdsObs always use the global early-exit form.
+bool expand_packs_records(const KgmtDev& d, int variant);
 void launch_expand(const KgmtDev& d, int t, int agent, int blocks, int variant, hipStream_t s,
                    const KernelTiming& tm = KernelTiming());
 // k_fold_r2: add the key log of iterations [tFirst, tLast] (at most kFoldEvery) to R2Valid / R2Invalid.

@@ -296,7 +296,7 @@ KgmtPlanner::KgmtPlanner(const sbmp_kgmt_params& p, int nranks, int rank, Exchan
     // (DESIGN.md §7), so the separate launch stays the default.  k_pack_x
     // (SBMP_EXCHANGE=fused) needs the separate pack.
     const char* pk = getenv("SBMP_PACK");
-    d.packInExpand = (d.sharded && !fusedPack_ && pk && std::string(pk) == "expand") ? 1 : 0;
+    packRequested_ = d.sharded && !fusedPack_ && pk && std::string(pk) == "expand";
 }
 
 KgmtPlanner::~KgmtPlanner() {
@@ -446,6 +446,7 @@ int KgmtPlanner::take_iteration() {
 }
 
 void KgmtPlanner::stage_expand(int t) {
+    if (d_.sharded) d_.packInExpand = (packRequested_ && expand_packs_records(d_, expandVariant_)) ? 1 : 0;
     launch_expand(d_, t, p_.agent, expandBlocks_, expandVariant_, stream_, timing(K_EXPAND));
 }
 

@@ -172,6 +172,7 @@ private:
     bool oneshot_ = false;                   // sharded: the exchange is k_oneshot over IPC-mapped inboxes
     unsigned long long* inbox_[kMaxRanks] = {nullptr};
     unsigned long long xSeq_ = 0;            // exchanges so far (the same count on every rank)
+    bool packRequested_ = false;             // SBMP_PACK=expand (k_expand packs in its register forms)
     bool fusedPack_ = false;                 // the exchange runs in k_pack's launch (k_pack_x)
     unsigned long long* arrive_ = nullptr;   // k_pack_x: per-packer flags (the exchange's seq)
     uint32_t* jumps_ = nullptr;
