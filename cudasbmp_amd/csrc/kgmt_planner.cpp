@@ -248,6 +248,7 @@ KgmtPlanner::KgmtPlanner(const sbmp_kgmt_params& p, int nranks, int rank, Exchan
     d.r2log = (d.nR2 <= kLogMaxR2) ? alloc<uint16_t>((size_t)kFoldEvery * d.logSlots) : nullptr;
     d.ctrl = alloc<IterCtrl>(p.numIterations + 2);
     d.status = alloc<PlannerStatus>(1);
+    SBMP_HIP(hipHostMalloc(reinterpret_cast<void**>(&poll_), sizeof(PollBuf), hipHostMallocDefault));
     d.timeline = nullptr;
     d.timelineFin = nullptr;
     d.timelineIter = -1;
@@ -310,6 +311,7 @@ KgmtPlanner::~KgmtPlanner() {
     }
     for (hipEvent_t e : eventPool_) (void)hipEventDestroy(e);
     for (void* ptr : allocs_) (void)hipFree(ptr);
+    if (poll_) (void)hipHostFree(poll_);
     if (obs_) (void)hipFree(obs_);
     if (gridStart_) (void)hipFree(gridStart_);
     if (gridBoxes_) (void)hipFree(gridBoxes_);
@@ -532,12 +534,17 @@ int KgmtPlanner::last_executed(const std::vector<IterCtrl>& c) const {
 
 bool KgmtPlanner::active() {
     if (!begun_) return false;
+    if (d_.stepMode && !flushed_) {   // the flush pass writes ctrl[t_next] and the goal of t_next - 1
+        launch_step(d_, t_next_, 0, p_.agent, expandVariant_, stream_, KernelTiming());
+        flushed_ = true;
+    }
+    // ctrl has numIterations + 2 entries, so t_next <= numIterations + 1 is in range
+    SBMP_HIP(hipMemcpyAsync(&poll_->ctrl, d_.ctrl + t_next_, sizeof(IterCtrl), hipMemcpyDeviceToHost, stream_));
+    SBMP_HIP(hipMemcpyAsync(&poll_->status, d_.status, sizeof(PlannerStatus), hipMemcpyDeviceToHost, stream_));
     sync();
     if (t_next_ > p_.numIterations) return false;
-    IterCtrl c;
-    PlannerStatus st;
-    SBMP_HIP(hipMemcpy(&c, d_.ctrl + t_next_, sizeof(IterCtrl), hipMemcpyDeviceToHost));
-    SBMP_HIP(hipMemcpy(&st, d_.status, sizeof(PlannerStatus), hipMemcpyDeviceToHost));
+    const IterCtrl c = poll_->ctrl;
+    const PlannerStatus st = poll_->status;
     if (st.error) throw Error(SBMP_ERR_HIP, "k_step: the plan hand-off timed out");
     // ctrl[t_next] was written by the last enqueued plan kernel: it says whether the
     // next iteration would run (tree not full, limit not reached); the goal ends it too.

@@ -162,6 +162,13 @@ private:
     int slotsPadded_ = 0, expandBlocks_ = 0, nbits_ = 1;
     int expandVariant_ = 0;   // SBMP_EXPAND_VARIANT: obstacle form, 0 = auto (3 if <= kMaxRegObs boxes, else 1)
     bool timelineDumped_ = false;
+    // Pinned host copy of (ctrl[t_next], status) for active(): both land with one
+    // stream synchronisation instead of two blocking copies per poll.
+    struct PollBuf {
+        IterCtrl ctrl;
+        PlannerStatus status;
+    };
+    PollBuf* poll_ = nullptr;
     bool flushed_ = true;     // k_step mode: the last enqueued iteration has been inserted
     int lastFolded_ = 0;      // iterations <= lastFolded_ are in R2Valid / R2Invalid
     unsigned long long* local_ = nullptr;   // sharded: the owner's block counts + GNew words
