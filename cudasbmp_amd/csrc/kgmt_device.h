@@ -81,7 +81,11 @@ constexpr int kStepEntry = 3;       // k_step list entry: state, (a, steer, dur,
 // k_step: when iteration t-1 accepted at most this many children, the planner
 // workgroup (idle once it has published) writes all of them into the tree, and the
 // expanding workgroups issue no insert loads or stores ahead of their propagation.
-constexpr int kPlannerInsertMax = 4096;
+// 1024 rather than 4096: the planner inserts 2 rows per thread per round behind a
+// binary search, so between 1,024 and 4,096 rows it became the launch's tail; the
+// driver's window measured +2.7% (13.58 vs 13.22 G samples/s mean, 5 run triples),
+// 300-step lines equal.
+constexpr int kPlannerInsertMax = 1024;
 constexpr int kStepPrefetch = 2;    // snapshot words per thread prefetched before propagation (nR2 <= 16,384)
 static_assert(kBlock / kWave == 4 && kMaxR1 == kBlock, "the flush and prefix code assumes 4 waves and 256 R1 cells");
 constexpr int kInsertBase = 8;   // k_finish workgroup of insert block 0 (one per XCD ahead of it)
