@@ -50,9 +50,18 @@ static_assert(sizeof(IterCtrl) == 64, "IterCtrl is one 64-B line");
 
 struct PlannerStatus {
     int goalIdx;    // lowest tree row inside the goal radius (kNoGoal if none), D4
-    int error;      // nonzero: a k_step hand-off timed out (the host raises it)
+    int error;      // nonzero: a bounded in-kernel wait gave up (kErr*; the host raises it)
     int pad[14];
 };
+// PlannerStatus::error: which bounded wait gave up.
+constexpr int kErrStepHandoff = 1;   // k_step: the planner workgroup's tagged scores/snapshot never arrived
+constexpr int kErrExchange = 2;      // k_oneshot: a peer rank's inbox flag never arrived
+// Bounds of those waits, in ticks of the 100 MHz s_memrealtime clock.  The in-launch
+// hand-off waits for a workgroup of the same launch (1 s); the exchange waits for
+// other processes, whose kernels may start seconds apart (startup, code loading,
+// per-iteration dumps), so it waits 20 s before it reports.
+constexpr long long kStepWaitTicks = 100000000ll;
+constexpr long long kExchangeWaitTicks = 2000000000ll;
 
 constexpr int kMaxLdsObs = 2048;     // obstacle lists up to 32 KB are staged in LDS per block
 // Obstacle-list forms of k_expand (template parameter OBS):
@@ -136,11 +145,6 @@ struct KgmtDev {
     int recCap;
     float4* recOut;
     const float4* recPeer[kMaxRanks];
-    // Sharded ranks with the pack folded into k_expand (packInExpand): per owned block,
-    // t << 33 | inclusive << 32 | count, published for the next blocks' look-back
-    // (DESIGN.md §7); zeroed by begin(), so tags of an earlier plan never match.
-    unsigned long long* packLook;
-    int packInExpand;
     // Region tables: R1, R1Avail, R1Valid, R1Invalid, R1Cov are the parity-0 slices
     // of one int array [2][5][nR1], R2Avail of [2][nR2/32].  k_finish updates parity
     // 0 in place; k_step (below) reads iteration t-1's parity and writes t's.

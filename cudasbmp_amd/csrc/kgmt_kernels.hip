@@ -106,67 +106,6 @@ __device__ __forceinline__ void store_record(float4* p, float4 v) {
                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-// Sharded ranks, k_pack folded into k_expand: the block's offset among
-// this rank's owned blocks is the sum of the earlier blocks' counts, which each block
-// publishes as t << 32 | count (one untorn 8-B store, self-validating by its tag);
-// the whole workgroup reads the earlier entries at once and re-reads until every tag
-// is t (earlier blocks were dispatched first and never wait on later ones).  Then the
-// records, the exchange's prefix fields and the rank total, as pack_block writes them.
-__device__ __forceinline__ void expand_pack(const KgmtDev& d, int t, const IterCtrl& c, int gblock, int cnt,
-                                            bool flagged, int idx, float4 cs, float4 cc) {
-    __shared__ int sPart[kBlock / kWave];
-    const int lb = (int)blockIdx.x;
-    const unsigned want = (unsigned)t;
-    unsigned long long* const look = d.packLook;
-    if (threadIdx.x == 0)
-        __hip_atomic_store(look + lb, (unsigned long long)want << 32 | (unsigned)cnt, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-    int part = 0;
-    if (lb > 0) {
-        const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
-        // Blocks finish roughly in dispatch order: one lane first waits for the block
-        // just before (one line), so the full read below mostly succeeds at once
-        // instead of every workgroup re-reading all earlier entries.
-        if (threadIdx.x == 0) {
-            while ((unsigned)(__hip_atomic_load(look + lb - 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >> 32) != want &&
-                   (long long)__builtin_amdgcn_s_memrealtime() - t0 <= 100000000ll)
-                __builtin_amdgcn_s_sleep(1);
-        }
-        __syncthreads();
-        for (;;) {
-            bool ok = true;
-            part = 0;
-            for (int i = (int)threadIdx.x; i < lb; i += kBlock) {
-                const unsigned long long v = __hip_atomic_load(look + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                ok &= (unsigned)(v >> 32) == want;
-                part += (int)(uint32_t)v;
-            }
-            if (__syncthreads_and(ok)) break;
-            // 1 s: report, do not hang (decided by a barrier, so every wave leaves together)
-            if (__syncthreads_or((long long)__builtin_amdgcn_s_memrealtime() - t0 > 100000000ll)) {
-                if (threadIdx.x == 0) atomicExch(&d.status->error, 1);
-                break;
-            }
-            __builtin_amdgcn_s_sleep(1);
-        }
-    }
-    part = wave_sum(part);
-    if ((threadIdx.x & (kWave - 1)) == 0) sPart[threadIdx.x >> 6] = part;
-    __syncthreads();
-    const int preLocal = sPart[0] + sPart[1] + sPart[2] + sPart[3];
-    if (flagged) {
-        float4* rec = d.recOut + ((size_t)(t & 1) * d.recCap + preLocal + idx) * kRecordF4;
-        store_record(rec, cs);
-        store_record(rec + 1, cc);
-        store_record(rec + 2, make_float4(__int_as_float(gblock), __int_as_float(idx), 0.0f, 0.0f));
-    }
-    const int next = gblock + d.nranks;   // H never decreases: blocks >= H never ran, entries past them are unused
-    const bool last = (long long)next * kBlock >= c.H;
-    const int hi = last ? d.nBlocks : min(next, d.nBlocks);
-    for (int g = gblock + 1 + (int)threadIdx.x; g <= hi; g += kBlock) d.pfxOut[g] = preLocal + cnt;
-    if (last && threadIdx.x == 0) d.totOut[d.rank] = preLocal + cnt;
-}
-
 // One thread per child slot, 256-slot workgroups.  Outputs: child state/controls/
 // parent (2 x 16 B), XORWOW state (16 + 8 B), GNew bits (one 8-B word per wave),
 // the GNew popcount of the workgroup, and the region bookkeeping of
@@ -181,7 +120,7 @@ __device__ __forceinline__ void expand_pack(const KgmtDev& d, int t, const IterC
 //               scattered device atomics run ~17x below the contiguous rate
 //               (MI355X_MICROARCH.md, global atomics); nothing reads these two
 //               arrays during the run (KGMT.cu:405,410 are write-only).
-template <int AGENT, int OBS, bool PACK = false>
+template <int AGENT, int OBS>
 __global__ __launch_bounds__(kBlock) void k_expand(KgmtDev d, int t) {
     extern __shared__ float4 sObs[];
     __shared__ float sScore[kMaxR1];
@@ -304,25 +243,6 @@ __global__ __launch_bounds__(kBlock) void k_expand(KgmtDev d, int t) {
     SBMP_STAMP(5);
     const int cntB = sWaveCnt[0] + sWaveCnt[1] + sWaveCnt[2] + sWaveCnt[3];
     if (tid == 0) d.blockCountOut[gblock] = cntB;
-    // Sharded rank with SBMP_PACK=expand: k_pack's work without its launch, in separate
-    // instantiations of the register obstacle forms (the host packs with k_pack
-    // otherwise): compiled into every form, the extra live state cost c5 3% (63.97 vs
-    // 61.9 us per k_expand at 1M children) and the register forms an occupancy step.
-    if constexpr (PACK) {
-        {
-            const unsigned long long now =   // this wave's GNew word, in every lane
-                ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)(oldWord >> 32), 0) << 32 |
-                 (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)oldWord, 0)) | mask;
-            int inBlock = 0;
-            for (int i = 0; i < wave; ++i) inBlock += sWaveCnt[i];
-            const bool flagged = (now >> lane) & 1ull;
-            if (__ballot(flagged && !act) != 0ull && flagged && !act) {   // a stale flag past S: the slot's last child
-                cs = d.uState[slot];
-                cc = d.uCtrl[slot];
-            }
-            expand_pack(d, t, c, gblock, cntB, flagged, inBlock + __popcll(now & ((1ull << lane) - 1ull)), cs, cc);
-        }
-    }
     {   // one 64-bit atomic per touched cell, into this workgroup's replica
         unsigned long long* const rep = d.deltaOut + (size_t)(blockIdx.x % kDeltaReps) * d.nR1;
         const int v = sR1P[tid];   // nR1 == kBlock
@@ -804,7 +724,6 @@ __device__ __forceinline__ void pack_block(const KgmtDev& d, int t) {
     const int next = gblock + d.nranks;   // H never decreases: blocks >= H never ran, entries past them are unused
     const bool last = (long long)next * kBlock >= c.H;
     const int hi = last ? d.nBlocks : min(next, d.nBlocks);
-    // written through (device scope): k_pack_x's exchange workgroups read them in this launch
     for (int g = gblock + 1 + (int)threadIdx.x; g <= hi; g += kBlock)
         __hip_atomic_store(d.pfxOut + g, preLocal + cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (last && threadIdx.x == 0)
@@ -866,9 +785,7 @@ constexpr int kOneshotChunks = 8;
 struct OneshotArgs {
     unsigned long long* inbox[kMaxRanks];
 };
-// Chunk c of the exchange.  coherentSend: `send` was written by other workgroups of
-// this launch (k_pack's fused form), so it is read with device-scope loads.
-template <bool kCoherentSend>
+// Chunk c of the exchange.
 __device__ __forceinline__ void oneshot_chunk(const OneshotArgs& a, const unsigned long long* __restrict__ send,
                                               unsigned long long* __restrict__ recv, long long n, int nranks,
                                               int rank, unsigned long long seq, int* error, int c) {
@@ -877,10 +794,7 @@ __device__ __forceinline__ void oneshot_chunk(const OneshotArgs& a, const unsign
     const size_t par = (size_t)(seq & 1ull) * nranks * n;
     const size_t flags = (size_t)2 * nranks * n;
     for (long long i = lo + threadIdx.x; i < hi; i += kBlock) {
-        const unsigned long long v =
-            kCoherentSend ? __hip_atomic_load(const_cast<unsigned long long*>(send) + i, __ATOMIC_RELAXED,
-                                              __HIP_MEMORY_SCOPE_AGENT)
-                          : send[i];
+        const unsigned long long v = send[i];
         for (int q = 0; q < nranks; ++q)
             __hip_atomic_store(a.inbox[q] + par + (size_t)rank * n + i, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
@@ -893,8 +807,8 @@ __device__ __forceinline__ void oneshot_chunk(const OneshotArgs& a, const unsign
         unsigned long long* f = a.inbox[rank] + flags + (size_t)q * kOneshotChunks + c;
         const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
         while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < seq) {
-            if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > 100000000ll) {   // 1 s: report, do not hang
-                atomicExch(error, 1);
+            if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > kExchangeWaitTicks) {   // report, do not hang
+                atomicExch(error, kErrExchange);
                 break;
             }
             __builtin_amdgcn_s_sleep(1);
@@ -914,51 +828,7 @@ __device__ __forceinline__ void oneshot_chunk(const OneshotArgs& a, const unsign
 __global__ __launch_bounds__(kBlock) void k_oneshot(OneshotArgs a, const unsigned long long* __restrict__ send,
                                                     unsigned long long* __restrict__ recv, long long n, int nranks,
                                                     int rank, unsigned long long seq, int* error) {
-    oneshot_chunk<false>(a, send, recv, n, nranks, rank, seq, error, (int)blockIdx.x);
-}
-
-// k_pack and the one-shot exchange in one launch: workgroups 0..nPack-1 pack (each
-// sets its flag arrive[b] = seq once its stores are visible device-wide), the last
-// kOneshotChunks workgroups -- dispatched after every packer -- wait until every
-// packer's flag reads seq, then exchange as k_oneshot does.  Saves a dependent launch
-// per iteration.
-struct PackXArgs {
-    OneshotArgs a;
-    const unsigned long long* send;   // this rank's exchange buffer (deltas first: d.deltaOut)
-    unsigned long long* recv;
-    long long n;
-    unsigned long long seq;
-    unsigned long long* arrive;   // [nPack] packer flags, monotone (seq)
-    int nPack;
-};
-__global__ __launch_bounds__(kBlock) void k_pack_x(KgmtDev d, int t, PackXArgs x) {
-    if ((int)blockIdx.x >= x.nPack) {
-        // every packer's flag: one word each (1,024 same-address device atomics would
-        // serialise at the memory side: 131 us per launch, measured)
-        const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
-        for (;;) {
-            bool ok = true;
-            for (int b = threadIdx.x; b < x.nPack; b += kBlock)
-                ok &= __hip_atomic_load(x.arrive + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= x.seq;
-            if (__syncthreads_and(ok)) break;
-            if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > 100000000ll) {   // uniform enough: all
-                if (threadIdx.x == 0) atomicExch(&d.status->error, 1);            // threads passed the barrier
-                break;
-            }
-            __builtin_amdgcn_s_sleep(1);
-        }
-        oneshot_chunk<true>(x.a, x.send, x.recv, x.n, d.nranks, d.rank, x.seq, &d.status->error,
-                            (int)blockIdx.x - x.nPack);
-        return;
-    }
-    pack_block(d, t);
-    // Its exchange-buffer and record stores are written through: once every wave's
-    // have completed, the flag may follow.  (__threadfence() would write back the whole
-    // L2 of the XCD, per packer: 127 us per launch, measured.)
-    __builtin_amdgcn_s_waitcnt(0);
-    __syncthreads();
-    if (threadIdx.x == 0)
-        __hip_atomic_store(x.arrive + blockIdx.x, x.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    oneshot_chunk(a, send, recv, n, nranks, rank, seq, error, (int)blockIdx.x);
 }
 
 size_t oneshot_inbox_words(long long n, int nranks) { return (size_t)2 * nranks * n + (size_t)nranks * kOneshotChunks; }
@@ -1466,13 +1336,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) voi
                     sNew[w] = 0u;
                 }
                 if (__syncthreads_and(ok)) break;
-                if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > 100000000ll) {   // 1 s: give up, report
+                if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > kStepWaitTicks) {   // give up, report
                     late = true;
                     break;
                 }
                 __builtin_amdgcn_s_sleep(8);
             }
-            if (late && tid == 0) atomicExch(&d.status->error, 1);
+            if (late && tid == 0) atomicExch(&d.status->error, kErrStepHandoff);
         }
     }
     SBMP_STAMP(4);
@@ -1707,18 +1577,18 @@ static void launch(K kernel, dim3 grid, dim3 block, size_t shm, hipStream_t s, c
         hipLaunchKernelGGL(kernel, grid, block, shm, s, args...);
 }
 
-template <int AGENT, bool PACK>
+template <int AGENT>
 static void launch_expand_reg(const KgmtDev& d, int t, dim3 grid, dim3 block, hipStream_t s, const KernelTiming& tm) {
     switch (d.nObs) {   // the box count is a compile-time constant of the register path
-        case 0: launch(k_expand<AGENT, kObsReg + 0, PACK>, grid, block, 0, s, tm, d, t); break;
-        case 1: launch(k_expand<AGENT, kObsReg + 1, PACK>, grid, block, 0, s, tm, d, t); break;
-        case 2: launch(k_expand<AGENT, kObsReg + 2, PACK>, grid, block, 0, s, tm, d, t); break;
-        case 3: launch(k_expand<AGENT, kObsReg + 3, PACK>, grid, block, 0, s, tm, d, t); break;
-        case 4: launch(k_expand<AGENT, kObsReg + 4, PACK>, grid, block, 0, s, tm, d, t); break;
-        case 5: launch(k_expand<AGENT, kObsReg + 5, PACK>, grid, block, 0, s, tm, d, t); break;
-        case 6: launch(k_expand<AGENT, kObsReg + 6, PACK>, grid, block, 0, s, tm, d, t); break;
-        case 7: launch(k_expand<AGENT, kObsReg + 7, PACK>, grid, block, 0, s, tm, d, t); break;
-        default: launch(k_expand<AGENT, kObsReg + 8, PACK>, grid, block, 0, s, tm, d, t); break;
+        case 0: launch(k_expand<AGENT, kObsReg + 0>, grid, block, 0, s, tm, d, t); break;
+        case 1: launch(k_expand<AGENT, kObsReg + 1>, grid, block, 0, s, tm, d, t); break;
+        case 2: launch(k_expand<AGENT, kObsReg + 2>, grid, block, 0, s, tm, d, t); break;
+        case 3: launch(k_expand<AGENT, kObsReg + 3>, grid, block, 0, s, tm, d, t); break;
+        case 4: launch(k_expand<AGENT, kObsReg + 4>, grid, block, 0, s, tm, d, t); break;
+        case 5: launch(k_expand<AGENT, kObsReg + 5>, grid, block, 0, s, tm, d, t); break;
+        case 6: launch(k_expand<AGENT, kObsReg + 6>, grid, block, 0, s, tm, d, t); break;
+        case 7: launch(k_expand<AGENT, kObsReg + 7>, grid, block, 0, s, tm, d, t); break;
+        default: launch(k_expand<AGENT, kObsReg + 8>, grid, block, 0, s, tm, d, t); break;
     }
 }
 
@@ -1732,19 +1602,12 @@ static void launch_expand_agent(const KgmtDev& d, int t, int blocks, int variant
     } else if (d.nObs > kMaxLdsObs) {
         launch(k_expand<AGENT, kObsGlobal>, grid, block, 0, s, tm, d, t);
     } else if (d.nObs <= kMaxRegObs && (variant == 0 || variant == 3)) {
-        if (d.packInExpand) launch_expand_reg<AGENT, true>(d, t, grid, block, s, tm);
-        else launch_expand_reg<AGENT, false>(d, t, grid, block, s, tm);
+        launch_expand_reg<AGENT>(d, t, grid, block, s, tm);
     } else if (variant == 2) {
         launch(k_expand<AGENT, kObsLds4>, grid, block, shm, s, tm, d, t);
     } else {
         launch(k_expand<AGENT, kObsLds>, grid, block, shm, s, tm, d, t);
     }
-}
-
-// k_expand packs the sharded records itself (SBMP_PACK=expand) only in its register
-// obstacle forms; launch_expand_agent picks one of those exactly in this case.
-bool expand_packs_records(const KgmtDev& d, int variant) {
-    return !d.gridStart && d.nObs <= kMaxLdsObs && d.nObs <= kMaxRegObs && (variant == 0 || variant == 3);
 }
 
 void launch_expand(const KgmtDev& d, int t, int agent, int blocks, int variant, hipStream_t s,
@@ -1808,20 +1671,6 @@ void launch_oneshot(unsigned long long* const* inbox, const unsigned long long* 
 
 void launch_finish(const KgmtDev& d, int t, int insertBlocks, hipStream_t s, const KernelTiming& tm) {
     launch(k_finish, dim3(1 + insertBlocks), dim3(kBlock), 0, s, tm, d, t);
-}
-
-void launch_pack_exchange(const KgmtDev& d, int t, int blocks, unsigned long long* const* inbox,
-                          const unsigned long long* send, unsigned long long* recv, long long n,
-                          unsigned long long seq, unsigned long long* arrive, hipStream_t s, const KernelTiming& tm) {
-    PackXArgs x{};
-    for (int q = 0; q < d.nranks; ++q) x.a.inbox[q] = inbox[q];
-    x.send = send;
-    x.recv = recv;
-    x.n = n;
-    x.seq = seq;
-    x.arrive = arrive;
-    x.nPack = blocks;
-    launch(k_pack_x, dim3(blocks + kOneshotChunks), dim3(kBlock), 0, s, tm, d, t, x);
 }
 
 void launch_pack(const KgmtDev& d, int t, int blocks, hipStream_t s, const KernelTiming& tm) {

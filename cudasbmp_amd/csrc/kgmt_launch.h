@@ -19,7 +19,6 @@ struct KernelTiming {
 // variant: obstacle form: 0 = auto, 1 = LDS rolled, 2 = LDS 4-way batched, 3 = registers
 // (lists of at most kMaxRegObs boxes; auto picks it there, else 1); lists longer
 // than kMaxLdsObs always use the global early-exit form.
-bool expand_packs_records(const KgmtDev& d, int variant);
 void launch_expand(const KgmtDev& d, int t, int agent, int blocks, int variant, hipStream_t s,
                    const KernelTiming& tm = KernelTiming());
 // k_fold_r2: add the key log of iterations [tFirst, tLast] (at most kFoldEvery) to R2Valid / R2Invalid.
@@ -37,15 +36,10 @@ void launch_pack(const KgmtDev& d, int t, int blocks, hipStream_t s, const Kerne
 // rank q's, oneshot_inbox_words() u64 each, zeroed once); seq = this exchange's number
 // in the plan's lifetime (1, 2, ...), the same on every rank.
 size_t oneshot_inbox_words(long long n, int nranks);
+// error: the planner's status word (set to kErrExchange when a peer never arrives).
 void launch_oneshot(unsigned long long* const* inbox, const unsigned long long* send, unsigned long long* recv,
                     long long n, int nranks, int rank, unsigned long long seq, int* error, hipStream_t s,
                     const KernelTiming& tm = KernelTiming());
-// k_pack and that exchange in one launch (blocks packers + the exchange workgroups);
-// arrive: blocks zeroed u64 packer flags kept for the planner's lifetime.
-void launch_pack_exchange(const KgmtDev& d, int t, int blocks, unsigned long long* const* inbox,
-                          const unsigned long long* send, unsigned long long* recv, long long n,
-                          unsigned long long seq, unsigned long long* arrive, hipStream_t s,
-                          const KernelTiming& tm = KernelTiming());
 // Local shard group: recv[q][i] = sum over ranks of send[r][i], for every rank q.
 void launch_xsum(const unsigned long long* const* send, unsigned long long* const* recv, int nranks, long long n,
                  hipStream_t s);

@@ -80,6 +80,15 @@ static float markstein_rcp(float b) {
     return y;
 }
 
+// PlannerStatus::error -> the bounded wait that gave up (kgmt_device.h kErr*).
+[[noreturn]] static void throw_wait_error(int e) {
+    if (e == kErrExchange)
+        throw Error(SBMP_ERR_COMM, "k_oneshot: a peer rank's exchange flag did not arrive within 20 s");
+    if (e == kErrStepHandoff)
+        throw Error(SBMP_ERR_HIP, "k_step: the planner workgroup's hand-off did not arrive within 1 s");
+    throw Error(SBMP_ERR_HIP, "in-kernel wait failed (status " + std::to_string(e) + ")");
+}
+
 static int round_up(long long x, long long m) { return (int)(((x + m - 1) / m) * m); }
 
 KgmtPlanner::KgmtPlanner(const sbmp_kgmt_params& p, int nranks, int rank, Exchange* ex, hipStream_t shared)
@@ -242,8 +251,6 @@ KgmtPlanner::KgmtPlanner(const sbmp_kgmt_params& p, int nranks, int rank, Exchan
     d.recOut = d.sharded ? alloc<float4>((size_t)2 * kRecordF4 * d.recCap) : nullptr;
     for (int q = 0; q < kMaxRanks; ++q) d.recPeer[q] = nullptr;
     d.recPeer[rank] = d.recOut;
-    d.packLook = d.sharded ? alloc<unsigned long long>(expandBlocks_) : nullptr;
-    d.packInExpand = 0;   // set below, once the exchange is chosen
     d.logSlots = expandBlocks_ * kBlock;
     d.r2log = (d.nR2 <= kLogMaxR2) ? alloc<uint16_t>((size_t)kFoldEvery * d.logSlots) : nullptr;
     d.ctrl = alloc<IterCtrl>(p.numIterations + 2);
@@ -271,33 +278,23 @@ KgmtPlanner::KgmtPlanner(const sbmp_kgmt_params& p, int nranks, int rank, Exchan
         for (int q = 0; q < nranks; ++q) d.recPeer[q] = static_cast<const float4*>(peers[q]);
         // The per-iteration exchange: a one-shot sum through IPC-mapped inboxes (the
         // default), or SBMP_EXCHANGE=collective for the Exchange's all-reduce (RCCL).
+        // Peers write the inboxes over xGMI while the owner's kernel polls them, so they
+        // are uncached device memory: a coarse-grained (hipMalloc) page may keep a stale
+        // line in the owner's L2, which only a kernel boundary refreshes.
         const char* v = getenv("SBMP_EXCHANGE");
         if (!(v && std::string(v) == "collective")) {
             const size_t words = oneshot_inbox_words((long long)xWords_, nranks);
-            unsigned long long* own = alloc<unsigned long long>(words);
+            void* own = nullptr;
+            SBMP_HIP(hipExtMallocWithFlags(&own, sizeof(unsigned long long) * words, hipDeviceMallocUncached));
+            allocs_.push_back(own);
             SBMP_HIP(hipMemset(own, 0, sizeof(unsigned long long) * words));
             SBMP_HIP(hipDeviceSynchronize());   // zeroed before any peer can see it
             void* ib[kMaxRanks] = {nullptr};
             ex_->share_buffer(own, sizeof(unsigned long long) * words, ib);
             for (int q = 0; q < nranks; ++q) inbox_[q] = static_cast<unsigned long long*>(ib[q]);
             oneshot_ = true;
-            arrive_ = alloc<unsigned long long>(expandBlocks_);
-            SBMP_HIP(hipMemset(arrive_, 0, sizeof(unsigned long long) * expandBlocks_));
-            SBMP_HIP(hipDeviceSynchronize());
-            // SBMP_EXCHANGE=fused: the exchange inside k_pack's launch (k_pack_x).  Two
-            // ranks sharing one GPU measured 12.2 vs 12.9 G samples/s for the separate
-            // launch, so the separate launch is the default.
-            fusedPack_ = v && std::string(v) == "fused";
         }
     }
-    // SBMP_PACK=expand: sharded ranks pack their records inside k_expand (each block
-    // sums the earlier owned blocks' published counts) instead of a k_pack launch.  A
-    // local group of 8 measured k_expand 16.6 us vs 13.3 + 4.5 us for k_expand + k_pack,
-    // one launch fewer; two ranks sharing one GPU measured 11.7 vs 12.6 G samples/s
-    // (DESIGN.md §7), so the separate launch stays the default.  k_pack_x
-    // (SBMP_EXCHANGE=fused) needs the separate pack.
-    const char* pk = getenv("SBMP_PACK");
-    packRequested_ = d.sharded && !fusedPack_ && pk && std::string(pk) == "expand";
 }
 
 KgmtPlanner::~KgmtPlanner() {
@@ -345,7 +342,6 @@ void KgmtPlanner::begin(const float* initial, const float* goal, const float* d_
         SBMP_HIP(hipMemsetAsync(d.stepR2New, 0, sizeof(uint32_t) * 3 * (d.nR2 / 32), s));
     }
     SBMP_HIP(hipMemsetAsync(d.R2Snap, 0, sizeof(uint32_t) * (d.nR2 / 32), s));
-    if (d.packLook) SBMP_HIP(hipMemsetAsync(d.packLook, 0, sizeof(unsigned long long) * expandBlocks_, s));
     SBMP_HIP(hipMemsetAsync(d.R2Valid, 0, sizeof(int) * d.nR2, s));
     SBMP_HIP(hipMemsetAsync(d.R2Invalid, 0, sizeof(int) * d.nR2, s));
     launch_fill_f32(d.R1Score, 1.0f, 2 * d.nR1, s);
@@ -413,6 +409,7 @@ void KgmtPlanner::begin(const float* initial, const float* goal, const float* d_
     begun_ = true;
     wallMs_ = 0.0;
     SBMP_HIP(hipStreamSynchronize(s));
+    if (ex_) ex_->barrier(s);   // every rank set up before the first (time-bounded) exchange
     t0_ = now_ms();
     if (d.stepMode) flushed_ = false;   // k_step(1) plans iteration 1 itself
     else launch_finish(d, 0, 0, s, timing(K_FINISH));   // prepares iteration 1
@@ -448,23 +445,15 @@ int KgmtPlanner::take_iteration() {
 }
 
 void KgmtPlanner::stage_expand(int t) {
-    if (d_.sharded) d_.packInExpand = (packRequested_ && expand_packs_records(d_, expandVariant_)) ? 1 : 0;
     launch_expand(d_, t, p_.agent, expandBlocks_, expandVariant_, stream_, timing(K_EXPAND));
 }
 
 void KgmtPlanner::stage_pack(int t) {
-    if (d_.packInExpand) return;   // k_expand packed already
-    if (oneshot_ && fusedPack_) {   // k_pack + the exchange in one launch (stage_exchange then does nothing)
-        ++xSeq_;
-        launch_pack_exchange(d_, t, expandBlocks_, inbox_, xSend_, xRecv_, (long long)xWords_, xSeq_, arrive_,
-                             stream_, timing(K_PACK));
-        return;
-    }
     launch_pack(d_, t, expandBlocks_, stream_, timing(K_PACK));
 }
 
 void KgmtPlanner::stage_exchange() {
-    if (!ex_ || (oneshot_ && fusedPack_)) return;
+    if (!ex_) return;
     if (oneshot_) {
         ++xSeq_;
         launch_oneshot(inbox_, xSend_, xRecv_, (long long)xWords_, d_.nranks, d_.rank, xSeq_, &d_.status->error,
@@ -545,7 +534,7 @@ bool KgmtPlanner::active() {
     if (t_next_ > p_.numIterations) return false;
     const IterCtrl c = poll_->ctrl;
     const PlannerStatus st = poll_->status;
-    if (st.error) throw Error(SBMP_ERR_HIP, "k_step: the plan hand-off timed out");
+    if (st.error) throw_wait_error(st.error);
     // ctrl[t_next] was written by the last enqueued plan kernel: it says whether the
     // next iteration would run (tree not full, limit not reached); the goal ends it too.
     return c.run && st.goalIdx == kNoGoal;
@@ -561,6 +550,7 @@ void Planner::run(int pollEvery) {
             for (const sbmp_iter_record& e : log)
                 if (e.itr > done) dump_iteration(dumpDir_, e.itr);
             if (!log.empty()) done = log.back().itr;
+            rank_barrier();   // the dump's host time must not count against a peer's exchange wait
             if (!active()) break;
         }
         sync();
@@ -579,7 +569,7 @@ void KgmtPlanner::result(sbmp_plan_result* r) {
     std::vector<IterCtrl> c;
     PlannerStatus st;
     read_ctrl(c, st);
-    if (st.error) throw Error(SBMP_ERR_HIP, "k_step: the plan hand-off timed out");
+    if (st.error) throw_wait_error(st.error);
     const int itr = last_executed(c);
     memset(r, 0, sizeof(*r));
     r->iterations = itr;

@@ -35,6 +35,10 @@ public:
     virtual void allreduce_i32(const int* send, int* recv, size_t n, hipStream_t s) = 0;
     // Every rank's device buffer of the same size, mapped into this process (IPC).
     virtual void share_buffer(void* own, size_t bytes, void* peers[kMaxRanks]) = 0;
+    // Returns once every rank has called it (host-side; `s` is drained first).  The
+    // one-shot exchange waits for its peers in-kernel with a time bound, so ranks are
+    // lined up here before their first exchange and after host-side pauses (dumps).
+    virtual void barrier(hipStream_t s) = 0;
 };
 
 // What the C ABI drives: one rank (single GPU or one rank of an RCCL group) or a
@@ -47,6 +51,7 @@ public:
     virtual void sync() = 0;
     virtual void fold_pending() = 0;   // enqueue k_fold_r2 up to the last enqueued iteration
     virtual bool active() = 0;   // syncs; false once the loop has ended
+    virtual void rank_barrier() {}   // sharded ranks: all ranks reach this point (Exchange::barrier)
     virtual void result(sbmp_plan_result* r) = 0;
     void run(int pollEvery);     // enqueue until the loop ends
     // Per-iteration dumps (reference KGMT.cu:263-290, commented out there; read by
@@ -105,6 +110,9 @@ public:
         if (begun_) fold_to(t_next_ - 1);
     }
     bool active() override;
+    void rank_barrier() override {
+        if (ex_) ex_->barrier(stream_);
+    }
     void result(sbmp_plan_result* r) override;
 
     hipStream_t stream() const override { return stream_; }
@@ -179,9 +187,6 @@ private:
     bool oneshot_ = false;                   // sharded: the exchange is k_oneshot over IPC-mapped inboxes
     unsigned long long* inbox_[kMaxRanks] = {nullptr};
     unsigned long long xSeq_ = 0;            // exchanges so far (the same count on every rank)
-    bool packRequested_ = false;             // SBMP_PACK=expand (k_expand packs in its register forms)
-    bool fusedPack_ = false;                 // the exchange runs in k_pack's launch (k_pack_x)
-    unsigned long long* arrive_ = nullptr;   // k_pack_x: per-packer flags (the exchange's seq)
     uint32_t* jumps_ = nullptr;
     float4* obs_ = nullptr;
     int obsCap_ = 0;

@@ -40,8 +40,10 @@ public:
         memcpy(&uid, id, sizeof(uid));
         SBMP_NCCL(ncclCommInitRank(&comm_, nranks, uid, rank));
         SBMP_HIP(hipStreamCreateWithFlags(&setup_, hipStreamNonBlocking));
+        SBMP_HIP(hipMalloc(&token_, sizeof(int)));
     }
     ~RcclExchange() override {
+        if (token_) (void)hipFree(token_);
         for (void* p : mapped_) (void)hipIpcCloseMemHandle(p);
         if (setup_) (void)hipStreamDestroy(setup_);
         if (comm_) (void)ncclCommDestroy(comm_);
@@ -52,6 +54,11 @@ public:
     }
     void allreduce_i32(const int* send, int* recv, size_t n, hipStream_t s) override {
         SBMP_NCCL(ncclAllReduce(send, recv, n, ncclInt32, ncclSum, comm_, s));
+    }
+    void barrier(hipStream_t s) override {   // a one-word all-reduce, waited for on the host
+        SBMP_HIP(hipStreamSynchronize(s));
+        SBMP_NCCL(ncclAllReduce(token_, token_, 1, ncclInt32, ncclSum, comm_, setup_));
+        SBMP_HIP(hipStreamSynchronize(setup_));
     }
     void share_buffer(void* own, size_t bytes, void* peers[kMaxRanks]) override {
         (void)bytes;
@@ -81,6 +88,7 @@ private:
     int nranks_, rank_;
     ncclComm_t comm_ = nullptr;
     hipStream_t setup_ = nullptr;
+    int* token_ = nullptr;
     std::vector<void*> mapped_;
 };
 
@@ -109,6 +117,14 @@ public:
             return c_.allreduce_i32(c_.ctx, static_cast<const int32_t*>(hs), static_cast<int32_t*>(hr), n);
         });
     }
+    void barrier(hipStream_t s) override {   // a one-int all-reduce through the callbacks
+        SBMP_HIP(hipSetDevice(device_));
+        SBMP_HIP(hipStreamSynchronize(s));
+        const int32_t one = 1;
+        int32_t sum = 0;
+        if (c_.allreduce_i32(c_.ctx, &one, &sum, 1) != 0 || sum != nranks_)
+            throw Error(SBMP_ERR_COMM, "host barrier (all-reduce callback) failed");
+    }
     void share_buffer(void* own, size_t bytes, void* peers[kMaxRanks]) override {
         (void)bytes;
         hipIpcMemHandle_t h;
@@ -133,8 +149,10 @@ private:
     void reduce(const void* send, void* recv, size_t bytes, hipStream_t s, F&& call) {
         SBMP_HIP(hipSetDevice(device_));
         if (2 * bytes > hostBytes_) {
-            if (host_) SBMP_HIP(hipHostFree(host_));
-            host_ = nullptr;
+            void* old = host_;
+            host_ = nullptr;   // cleared first: a throw below leaves nothing to free twice
+            hostBytes_ = 0;
+            if (old) (void)hipHostFree(old);
             SBMP_HIP(hipHostMalloc(&host_, 2 * bytes));
             hostBytes_ = 2 * bytes;
         }

@@ -242,25 +242,6 @@ def test_local_shard_group_bit_exact(P, kw, seed, d_obs, obstacles, oracle_lib):
     assert_same_state(g, o, label=f"P={P} {kw}")
 
 
-@pytest.mark.parametrize("P,kw,seed", [
-    (3, dict(), 2),
-    (8, dict(samplesPerIteration=8192, batchRule="fill", maxTreeSize=300000, numIterations=12, goalThreshold=0.0), 7),
-])
-def test_local_shard_group_pack_in_expand_bit_exact(P, kw, seed, d_obs, obstacles, oracle_lib, monkeypatch):
-    """SBMP_PACK=expand: the records packed inside k_expand (each block sums the earlier
-    owned blocks' published counts) instead of by a k_pack launch, same results."""
-    from cudasbmp_amd import KGMT
-    monkeypatch.setenv("SBMP_PACK", "expand")
-    cfg = dict(DEMO)
-    extra = {k: kw[k] for k in ("samplesPerIteration", "agent", "fixGNewClear", "batchRule") if k in kw}
-    cfg.update({k: v for k, v in kw.items() if k not in extra})
-    g = KGMT(**cfg, **extra, _local_group=P)
-    g.plan(DEMO_INITIAL, DEMO_GOAL, d_obs, len(obstacles), seed=seed)
-    o = _oracle(cfg, extra)
-    o.plan(DEMO_INITIAL, DEMO_GOAL, obstacles, seed)
-    assert_same_state(g, o, label=f"P={P} pack in k_expand {kw}")
-
-
 def test_rccl_single_rank_sharded_path(d_obs, obstacles, oracle_lib):
     """The RCCL rank path end to end on one GPU: ncclCommInitRank, the fused
     ncclAllReduce per iteration, the IPC record-buffer exchange (own buffer) and

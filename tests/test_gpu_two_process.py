@@ -6,9 +6,8 @@ read by the peer over HIP IPC (hipIpcGetMemHandle / hipIpcOpenMemHandle, handles
 exchanged by an allgather), and the fused exchange buffer all-reduced every
 iteration, either by the default one-shot exchange (each rank stores its buffer into
 every rank's IPC-mapped inbox and raises flags; both processes' kernels meet on the
-GPU) as its own k_oneshot launch or, with SBMP_EXCHANGE=fused, inside k_pack's launch
-(k_pack_x), or, with SBMP_EXCHANGE=collective, by the Exchange's all-reduce; with
-SBMP_PACK=expand the records are packed inside k_expand instead of by k_pack.
+GPU; the inboxes are uncached device memory) as its own k_oneshot launch, or, with
+SBMP_EXCHANGE=collective, by the Exchange's all-reduce.
 RCCL cannot put two ranks on one device, so that all-reduce and the IPC handle
 exchange run over torch.distributed gloo through the host-collectives seam
 (cudasbmp_amd/host_comm.py).  The ranks' merged state must equal the CPU oracle's
@@ -37,14 +36,10 @@ def _free_port():
 def _rank_main(rank, port, kw, seed, out_dir, exchange):
     import sys
     sys.path.insert(0, ROOT)
-    if exchange in ("collective", "fused"):
+    if exchange == "collective":
         os.environ["SBMP_EXCHANGE"] = exchange
     else:
         os.environ.pop("SBMP_EXCHANGE", None)
-    if exchange == "expand":   # one-shot exchange, records packed inside k_expand
-        os.environ["SBMP_PACK"] = "expand"
-    else:
-        os.environ.pop("SBMP_PACK", None)
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     import torch.distributed as dist
@@ -75,8 +70,6 @@ def _rank_main(rank, port, kw, seed, out_dir, exchange):
     (dict(samplesPerIteration=4096, batchRule="fill", maxTreeSize=200000, numIterations=15, goalThreshold=0.0), 21,
      "oneshot"),
     (dict(fixGNewClear=True, numIterations=40), 8, "oneshot"),
-    (dict(fixGNewClear=True, numIterations=40), 8, "fused"),
-    (dict(fixGNewClear=True, numIterations=40), 8, "expand"),
     (dict(), 3, "collective"),
     (dict(samplesPerIteration=4096, batchRule="fill", maxTreeSize=200000, numIterations=15, goalThreshold=0.0), 21,
      "collective"),

@@ -30,24 +30,6 @@ __global__ __launch_bounds__(256) void k_valu(float* out, int iters) {
     if (s == 12345.f) out[threadIdx.x] = s;
 }
 
-// SALU mixed in: one s_and_b64 per v_fma_f32 (as the box tests do)
-__global__ __launch_bounds__(256) void k_mix(float* out, int iters) {
-    float a[8];
-    for (int i = 0; i < 8; ++i) a[i] = threadIdx.x * 1e-3f + i;
-    const float b = 0.999f, c = 1e-4f;
-    unsigned long long m = 0x5555ull;
-    for (int it = 0; it < iters; ++it) {
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            asm volatile("v_fma_f32 %0, %0, %1, %2" : "+v"(a[i]) : "v"(b), "v"(c));
-            asm volatile("s_and_b64 %0, %0, %1" : "+s"(m) : "s"(0x7777ull));
-        }
-    }
-    float s = (float)m;
-    for (int i = 0; i < 8; ++i) s += a[i];
-    if (s == 12345.f) out[threadIdx.x] = s;
-}
-
 int main() {
     setvbuf(stdout, nullptr, _IONBF, 0);
     printf("start\n");
@@ -56,22 +38,21 @@ int main() {
     hipEvent_t e0, e1;
     hipEventCreate(&e0);
     hipEventCreate(&e1);
-    const int iters = 4096;
-    for (int variant = 0; variant < 3; ++variant) {
+    const int iters = 32768;   // ~0.5 ms per launch at 1 wave per SIMD: launch overhead < 1%
+    for (int variant = 0; variant < 2; ++variant) {
         for (int w = 1; w <= 8; w *= 2) {
             const dim3 grid(256 * w);   // 256-thread workgroups: one wave per SIMD per workgroup
             for (int rep = 0; rep < 3; ++rep) {
                 hipEventRecord(e0);
                 if (variant == 0) hipLaunchKernelGGL(k_valu<0>, grid, dim3(256), 0, 0, out, iters);
-                else if (variant == 1) hipLaunchKernelGGL(k_valu<1>, grid, dim3(256), 0, 0, out, iters);
-                else hipLaunchKernelGGL(k_mix, grid, dim3(256), 0, 0, out, iters);
+                else hipLaunchKernelGGL(k_valu<1>, grid, dim3(256), 0, 0, out, iters);
                 hipEventRecord(e1);
                 hipEventSynchronize(e1);
             }
             float ms;
             hipEventElapsedTime(&ms, e0, e1);
             const double instr = (double)iters * 8 * w;   // VALU instructions per SIMD
-            const char* name = variant == 0 ? "v_fma_f32" : variant == 1 ? "v_pk_fma_f32" : "v_fma_f32+s_and_b64";
+            const char* name = variant == 0 ? "v_fma_f32" : "v_pk_fma_f32";
             printf("%-22s waves/SIMD %d: %.3f ms, %.2f ns per VALU instr per SIMD (%.2f cycles @2.4GHz)\n", name, w, ms,
                    ms * 1e6 / instr, ms * 1e6 / instr * 2.4);
         }
