@@ -15,6 +15,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "sbmp/collision.h"
 #include "sbmp/grid.h"
 #include "sbmp/obstacle_grid.h"
@@ -95,7 +97,6 @@ constexpr int kStepEntry = 3;       // k_step list entry: state, (a, steer, dur,
 // driver's window measured +2.7% (13.58 vs 13.22 G samples/s mean, 5 run triples),
 // 300-step lines equal.
 constexpr int kPlannerInsertMax = 1024;
-constexpr int kStepPrefetch = 2;    // snapshot words per thread prefetched before propagation (nR2 <= 16,384)
 static_assert(kBlock / kWave == 4 && kMaxR1 == kBlock, "the flush and prefix code assumes 4 waves and 256 R1 cells");
 constexpr int kInsertBase = 8;   // k_finish workgroup of insert block 0 (one per XCD ahead of it)
 constexpr int kRecordF4 = 3;   // sharded record: state, ctrl (a, steer, dur, parent), (block, index in block, -, -)
@@ -393,6 +394,19 @@ __device__ __forceinline__ void sincos_pred(float x, float* s, float* c) {
     }
 }
 
+// tanf_d for a steering angle: (float)fma(2u, pi, -pi) with u in (0, 1] lies in
+// (-pi, pi], so reduce_pio2 always takes its Cody-Waite branch and the argument is
+// finite: the non-finite and Payne-Hanek paths of tanf_d are dead here, and the
+// result is bitwise tanf_d's (same operations on the same reduced value).
+__device__ __forceinline__ float tan_steer(float x) {
+    const float j = __builtin_rintf(x * 0.636619772f);
+    float r = __builtin_fmaf(j, -1.57079601e+00f, x);
+    r = __builtin_fmaf(j, -3.13916473e-07f, r);
+    r = __builtin_fmaf(j, -5.39030253e-15f, r);
+    const float t = tan_poly(r);
+    return ((int)j & 1) ? -1.0f / t : t;
+}
+
 // Wave-level culling of the per-step tests (register obstacle lists).  Every
 // segment box of a child lies inside the square of half-width R around its start
 // (sup |displacement| over the steps, plus a margin far above the rounding of the
@@ -446,22 +460,45 @@ struct NoMidHook {
     __device__ void operator()() const {}
 };
 
+// The controls of one child (statePropagator.cu:17-21): they depend on the slot's
+// XORWOW stream only, not on the parent, so k_step draws them while its block counts
+// are still in flight.  car: (a, steering, duration, dt, tan(steering));
+// point: (vx, vy, duration, dt).
+struct ChildCtl {
+    float a, steer, dur, dt, tanS;
+};
+
+template <int AGENT>
+__device__ __forceinline__ ChildCtl draw_controls(Xorwow& rs, const KgmtDev& d) {
+    ChildCtl c;
+    if (AGENT == 0) {
+        c.a = __builtin_fmaf(xorwow_uniform(rs), 10.0f, -5.0f);
+        const float u2 = xorwow_uniform(rs);
+        c.steer = (float)__builtin_fma((double)(u2 * 2.0f), 3.141592653589793, -3.141592653589793);
+        c.dur = __builtin_fmaf(xorwow_uniform(rs), 1.0f, 0.05f);
+        c.dt = div_or_ieee(c.dur, (float)d.numDisc, d.rcpNumDisc);
+        c.tanS = tan_steer(c.steer);
+    } else {
+        c.a = __builtin_fmaf(xorwow_uniform(rs), 2.0f, -1.0f);      // vx
+        c.steer = __builtin_fmaf(xorwow_uniform(rs), 2.0f, -1.0f);  // vy
+        c.dur = __builtin_fmaf(xorwow_uniform(rs), 1.0f, 0.05f);
+        c.dt = div_or_ieee(c.dur, (float)d.numDisc, d.rcpNumDisc);
+        c.tanS = 0.0f;
+    }
+    return c;
+}
+
 // midHook() runs once, before Euler step numDisc / 2, on every lane that entered (k_step
 // issues the planner-publication loads there: late enough to see them, early enough
 // that they have landed when propagation ends).
 template <int OBS, typename MidHook = NoMidHook>
-__device__ __forceinline__ bool propagate_car(float4 p, Xorwow& rs, const KgmtDev& d, const float4* obs,
-                                              ChildOut& out, MidHook midHook = MidHook()) {
-    const float a = __builtin_fmaf(xorwow_uniform(rs), 10.0f, -5.0f);
-    const float u2 = xorwow_uniform(rs);
-    const float steering = (float)__builtin_fma((double)(u2 * 2.0f), 3.141592653589793, -3.141592653589793);
-    const float duration = __builtin_fmaf(xorwow_uniform(rs), 1.0f, 0.05f);
-    const float dt = div_or_ieee(duration, (float)d.numDisc, d.rcpNumDisc);
+__device__ __forceinline__ bool car_euler(float4 p, const ChildCtl& ctl, const KgmtDev& d, const float4* obs,
+                                          ChildOut& out, MidHook midHook = MidHook()) {
+    const float a = ctl.a, duration = ctl.dur, dt = ctl.dt, tan_steering = ctl.tanS;
     // (x, y) and (theta, v) as float pairs: each pair update is one v_pk_mul_f32 /
     // v_pk_fma_f32 doing the same IEEE operation per component (same bits).
     sbmp_f32x2 xy = {p.x, p.y}, tv = {p.z, p.w};
     const sbmp_f32x2 dt2 = {dt, dt};
-    const float tan_steering = tanf_d(steering);
     // |v| <= |v0| + |a| t, so the displacement stays below T |v0| + |a| T^2 / 2.
     WaveCull cull{~0u, true};
     if (OBS >= kObsReg) {
@@ -469,7 +506,9 @@ __device__ __forceinline__ bool propagate_car(float4 p, Xorwow& rs, const KgmtDe
         cull = wave_cull<OBS>(p.x, p.y, r, r, obs, d);
     }
     bool alive = true;
-    auto step = [&]() {
+    // v / L: one multiply when L is a power of two (invAgentLength != 0), else div_by
+    // with an IEEE fallback.  The choice is per plan, so the loop is unswitched on it.
+    auto step = [&](auto invL) {
         if (!alive) return;
         float st, ct;
         sincos_pred(tv.x, &st, &ct);
@@ -479,7 +518,7 @@ __device__ __forceinline__ bool propagate_car(float4 p, Xorwow& rs, const KgmtDe
         const bool oob = cull.bounds && ((seg_min(nx, ny) <= 0.0f) | (nx >= d.width) | (ny >= d.height));
         const float v = tv.y;
         float vl;
-        if (d.invAgentLength != 0.0f) {
+        if (decltype(invL)::value) {
             vl = v * d.invAgentLength;
         } else {
             vl = div_by(v, d.agentLength, d.rcpAgentLength);
@@ -506,25 +545,27 @@ __device__ __forceinline__ bool propagate_car(float4 p, Xorwow& rs, const KgmtDe
     };
     // two loops around the hook: no per-step test of the step index
     const int midStep = d.numDisc >> 1;
-    for (int i = 0; i < midStep; ++i) step();
-    midHook();
-    for (int i = midStep; i < d.numDisc; ++i) step();
-    const float x = xy.x, y = xy.y, theta = tv.x, v = tv.y;
-    out.state = make_float4(x, y, theta, v);
+    if (d.invAgentLength != 0.0f) {
+        for (int i = 0; i < midStep; ++i) step(std::true_type());
+        midHook();
+        for (int i = midStep; i < d.numDisc; ++i) step(std::true_type());
+    } else {
+        for (int i = 0; i < midStep; ++i) step(std::false_type());
+        midHook();
+        for (int i = midStep; i < d.numDisc; ++i) step(std::false_type());
+    }
+    out.state = make_float4(xy.x, xy.y, tv.x, tv.y);
     out.a = a;
-    out.steer = steering;
+    out.steer = ctl.steer;
     out.dur = duration;
     return alive;
 }
 
-// Holonomic R2 point (build extension), predicated like propagate_car.
+// Holonomic R2 point (build extension), predicated like car_euler.
 template <int OBS, typename MidHook = NoMidHook>
-__device__ __forceinline__ bool propagate_point(float4 p, Xorwow& rs, const KgmtDev& d, const float4* obs,
-                                                ChildOut& out, MidHook midHook = MidHook()) {
-    const float vx = __builtin_fmaf(xorwow_uniform(rs), 2.0f, -1.0f);
-    const float vy = __builtin_fmaf(xorwow_uniform(rs), 2.0f, -1.0f);
-    const float duration = __builtin_fmaf(xorwow_uniform(rs), 1.0f, 0.05f);
-    const float dt = div_or_ieee(duration, (float)d.numDisc, d.rcpNumDisc);
+__device__ __forceinline__ bool point_euler(float4 p, const ChildCtl& ctl, const KgmtDev& d, const float4* obs,
+                                            ChildOut& out, MidHook midHook = MidHook()) {
+    const float vx = ctl.a, vy = ctl.steer, duration = ctl.dur, dt = ctl.dt;
     float x = p.x, y = p.y;
     WaveCull cull{~0u, true};
     if (OBS >= kObsReg)
@@ -535,7 +576,7 @@ __device__ __forceinline__ bool propagate_point(float4 p, Xorwow& rs, const Kgmt
         const float nx = __builtin_fmaf(vx, dt, x);
         const float ny = __builtin_fmaf(vy, dt, y);
         const bool oob = cull.bounds && ((seg_min(nx, ny) <= 0.0f) | (nx >= d.width) | (ny >= d.height));
-        const float minx = seg_min(x, nx), maxx = seg_max(x, nx);   // see propagate_car
+        const float minx = seg_min(x, nx), maxx = seg_max(x, nx);   // see car_euler
         const float miny = seg_min(y, ny), maxy = seg_max(y, ny);
         bool freeSeg;
         if (OBS >= kObsReg) freeSeg = motion_valid_culled<OBS>(minx, miny, maxx, maxy, obs, cull.boxes);
@@ -556,6 +597,21 @@ __device__ __forceinline__ bool propagate_point(float4 p, Xorwow& rs, const Kgmt
     out.steer = vy;
     out.dur = duration;
     return alive;
+}
+
+// reference statePropagator.cu:5-76: controls, then the Euler loop (k_expand's form).
+template <int OBS, typename MidHook = NoMidHook>
+__device__ __forceinline__ bool propagate_car(float4 p, Xorwow& rs, const KgmtDev& d, const float4* obs,
+                                              ChildOut& out, MidHook midHook = MidHook()) {
+    const ChildCtl c = draw_controls<0>(rs, d);
+    return car_euler<OBS>(p, c, d, obs, out, midHook);
+}
+
+template <int OBS, typename MidHook = NoMidHook>
+__device__ __forceinline__ bool propagate_point(float4 p, Xorwow& rs, const KgmtDev& d, const float4* obs,
+                                                ChildOut& out, MidHook midHook = MidHook()) {
+    const ChildCtl c = draw_controls<1>(rs, d);
+    return point_euler<OBS>(p, c, d, obs, out, midHook);
 }
 
 }  // namespace sbmp

@@ -311,8 +311,8 @@ __device__ __forceinline__ void batch_rule(const KgmtDev& d, int treeSize, int n
     long long remaining = (long long)d.M - treeSize;
     if (d.cap > 0 && remaining > d.cap) remaining = d.cap;
     if (d.cap > 0 && d.batchRule == 1) {   // D14: fill the batch
-        if (nG <= remaining) {
-            *k = (int)(remaining / nG);
+        if (nG <= remaining) {   // 1 <= remaining <= M - 1 < 2^31: a 32-bit quotient
+            *k = (remaining < kFastDivMax) ? div_small((int)remaining, nG) : (int)remaining / nG;
             *nExp = nG;
         } else {
             *k = 1;
@@ -1118,18 +1118,26 @@ __device__ __forceinline__ void step_planner(const KgmtDev& d, int t, int expand
 }
 
 // 5 waves per SIMD: the 1 + nBlocks workgroups (1,025 at 262,144 slots) fit the chip at once.
+// The expanding workgroups:
+//   prologue   RNG / count / control-block loads, then the child's controls (they need
+//              the slot's stream only) while the counts are in flight; the count scan,
+//              the plan scalars, the D6 clear, the parent (list search);
+//   propagate  the Euler loop (statePropagator.cu:23-65);
+//   accept     each lane reads the two published words it needs (score of its R1 cell,
+//              snapshot word of its R2 cell, tagged with t) straight from L2, with no
+//              LDS staging and no barrier; stores overlap that round trip;
+//   epilogue   one barrier: wave counts -> list positions, the R1 / R2New flushes and
+//              the block's packed count.
 template <int AGENT, int OBS>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) void k_step(KgmtDev d, int t,
                                                                                         int expand) {
     extern __shared__ float4 sDyn[];   // [LDS obstacles][prefix: nBlocks + 1 ints]
-    __shared__ float sScore[kMaxR1];
     __shared__ int sR1P[kMaxR1];
-    __shared__ uint32_t sSnap[kMaxR2Words];
     __shared__ uint32_t sNew[kMaxR2Words];
     __shared__ int sWaveCnt[kBlock / kWave];
+    __shared__ int sWaveGoal[kBlock / kWave];
     __shared__ int sRed[2][kBlock / kWave];
     __shared__ float sPart[8];
-    __shared__ int sStale;
     __shared__ int sCovInc[kMaxR1];
 
     constexpr bool kLdsObs = (OBS == kObsLds || OBS == kObsLds4);
@@ -1147,7 +1155,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) voi
     const int slot = b * kBlock + tid;
     const int nW = d.nR2 >> 5;
     const int pp = (t - 1) & 1, cp = t & 1;
-    unsigned long long* const pubCur = d.stepPub + (size_t)cp * (d.nR1 + nW);
+    const unsigned long long* const pubCur = d.stepPub + (size_t)cp * (d.nR1 + nW);
     long long* const tl = (d.timeline && t == d.timelineIter && expand)
                               ? d.timeline + ((size_t)b * (kBlock / kWave) + wave) * kTimelineStamps
                               : nullptr;
@@ -1168,7 +1176,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) voi
     const unsigned long long oldWord = (lane == 0) ? d.gnewOut[slot >> 6] : 0ull;
     const float4 obsReg = (kLdsObs && tid < d.nObs) ? d.obstacles[tid] : make_float4(0.f, 0.f, 0.f, 0.f);
     sR1P[tid] = 0;   // nR1 == kBlock
-    if (tid == 0) sStale = 0;
+    for (int i = tid; i < nW; i += kBlock) sNew[i] = 0u;
+    // ---- the child's controls (statePropagator.cu:17-21) depend on the slot's stream
+    // alone: drawn while the block counts are in flight (stored only for slots < S)
+    Xorwow rs{ra.x, ra.y, ra.z, ra.w, rb.x, rb.y};
+    const ChildCtl ctl = draw_controls<AGENT>(rs, d);
     int A, jGoal;
     step_scan(d, pk, sPfx, sRed, &A, &jGoal);
     SBMP_STAMP(1);
@@ -1251,33 +1263,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) voi
             srcCost = reinterpret_cast<const float*>(src + 2);
         }
     }
-    // Parent, obstacles (and, for the global-list and grid variants, the planner's
-    // published scores and snapshot of t, checked after propagation) are issued back to
-    // back and waited for together.  The prefetch addresses are clamped instead of predicated: a load under a divergent
-    // branch makes the wait ahead of propagation a full vmcnt(0).
+    // Parent and obstacles are issued back to back and waited for together.
     const float4 p = *src;
     const float parentCost = *srcCost;
     float4 ro[kRegObs > 0 ? kRegObs : 1];
 #pragma unroll
     for (int i = 0; i < kRegObs; ++i) ro[i] = d.obstacles[i];
-    const bool pre = nW <= kStepPrefetch * kBlock;
-    unsigned long long pubS = 0ull, pubW[kStepPrefetch];
-    auto loadPub = [&]() {
-        if (pre) {
-            pubS = __hip_atomic_load(pubCur + min(tid, d.nR1 - 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#pragma unroll
-            for (int j = 0; j < kStepPrefetch; ++j)
-                pubW[j] = __hip_atomic_load(pubCur + d.nR1 + min(tid + j * kBlock, nW - 1), __ATOMIC_RELAXED,
-                                            __HIP_MEMORY_SCOPE_AGENT);
-        }
-    };
-    // The planner publishes ~3 us into the launch, about when the waves start
-    // propagating: loaded here, half the workgroups saw stale tags and paid a re-read
-    // round trip after propagation.  Variants without global loads in the Euler loop
-    // issue them at its midpoint instead (a global load there would make the loop's own
-    // waits cover them); lanes past S, which do not propagate, load after it.
-    constexpr bool kMidPub = kRegObs > 0 || kLdsObs;
-    if (!kMidPub) loadPub();
     insert_prev();
     if (kLdsObs) {
         if (tid < d.nObs) sObs[tid] = obsReg;
@@ -1286,81 +1277,31 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) voi
     }
     SBMP_STAMP(2);
     const float4* obs = (kRegObs > 0) ? ro : kLdsObs ? sObs : d.obstacles;
-    Xorwow rs{ra.x, ra.y, ra.z, ra.w, rb.x, rb.y};
     ChildOut out;
     bool valid = false;
-    if (kMidPub) {
-        if (act)
-            valid = (AGENT == 0) ? propagate_car<OBS>(p, rs, d, obs, out, loadPub)
-                                 : propagate_point<OBS>(p, rs, d, obs, out, loadPub);
-        else loadPub();
-    } else if (act) {
-        valid = (AGENT == 0) ? propagate_car<OBS>(p, rs, d, obs, out) : propagate_point<OBS>(p, rs, d, obs, out);
-    }
+    if (act) valid = (AGENT == 0) ? car_euler<OBS>(p, ctl, d, obs, out) : point_euler<OBS>(p, ctl, d, obs, out);
     SBMP_STAMP(3);
-    {   // tags must read t; re-read (bounded) what the prefetch got too early
-        const unsigned want = (unsigned)t;
-        bool ok = pre;
-        if (pre) {
-            if (tid < d.nR1) {
-                ok &= (unsigned)(pubS >> 32) == want;
-                sScore[tid] = __uint_as_float((uint32_t)pubS);
-            }
-#pragma unroll
-            for (int j = 0; j < kStepPrefetch; ++j) {
-                const int w = tid + j * kBlock;
-                if (w < nW) {
-                    ok &= (unsigned)(pubW[j] >> 32) == want;
-                    sSnap[w] = (uint32_t)pubW[j];
-                    sNew[w] = 0u;
-                }
-            }
-        }
-        if (__ballot(!ok) != 0ull && lane == 0) sStale = 1;   // one barrier, not __syncthreads_and's three
-        __syncthreads();
-        if (sStale) {
-            const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
-            bool late = false;
-            for (;;) {
-                ok = true;
-                if (tid < d.nR1) {
-                    const unsigned long long v = __hip_atomic_load(pubCur + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    ok &= (unsigned)(v >> 32) == want;
-                    sScore[tid] = __uint_as_float((uint32_t)v);
-                }
-                for (int w = tid; w < nW; w += kBlock) {
-                    const unsigned long long v =
-                        __hip_atomic_load(pubCur + d.nR1 + w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    ok &= (unsigned)(v >> 32) == want;
-                    sSnap[w] = (uint32_t)v;
-                    sNew[w] = 0u;
-                }
-                if (__syncthreads_and(ok)) break;
-                if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > kStepWaitTicks) {   // give up, report
-                    late = true;
-                    break;
-                }
-                __builtin_amdgcn_s_sleep(8);
-            }
-            if (late && tid == 0) atomicExch(&d.status->error, kErrStepHandoff);
-        }
+
+    // ---- bins (KGMT.cu:390-391) and the accept test (KGMT.cu:394-411, D2)
+    int q1 = -1, q2 = -1;
+    if (act) {
+        q1 = getR1_k(out.state.x, out.state.y, d.R1Size, d.rcpR1Size, kN);   // N = 16 (KGMT.cu:8)
+        q2 = getR2_k(out.state.x, out.state.y, q1, d.R1Size, kN, d.R2Size, d.rcpR2Size, d.n);
     }
-    SBMP_STAMP(4);
-    bool accept = false;
+    // The planner workgroup publishes iteration t's scores and snapshot as 8-B words
+    // tagged with t (step_planner); each lane that takes the test reads its two words
+    // from L2 now, and the stores below overlap that round trip.  q2 >= 0 implies q1 >= 0.
+    const bool look = act && valid && q2 >= 0;
+    unsigned long long sw = 0ull, aw = 0ull;
+    if (look) {
+        sw = __hip_atomic_load(pubCur + q1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        aw = __hip_atomic_load(pubCur + d.nR1 + (q2 >> 5), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    float u = 0.0f;
     float4 cs = make_float4(0.f, 0.f, 0.f, 0.f), cc = cs;   // this slot's child (state, ctrl)
     float cost = 0.0f;
     if (act) {
-        const int q1 = getR1_k(out.state.x, out.state.y, d.R1Size, d.rcpR1Size, kN);   // N = 16 (KGMT.cu:8)
-        const int q2 = getR2_k(out.state.x, out.state.y, q1, d.R1Size, kN, d.R2Size, d.rcpR2Size, d.n);
-        if (valid) {
-            const float u = xorwow_uniform(rs);   // KGMT.cu:395
-            if (q2 >= 0) {
-                const uint32_t bit = 1u << (q2 & 31);
-                const bool r2Avail = sSnap[q2 >> 5] & bit;
-                accept = (u <= sScore[q1]) || !r2Avail;
-                if (!r2Avail) atomicOr(&sNew[q2 >> 5], bit);
-            }
-        }
+        if (valid) u = xorwow_uniform(rs);   // KGMT.cu:395
         cs = out.state;
         cc = make_float4(out.a, out.steer, out.dur, __int_as_float(parent));
         cost = parentCost + out.dur;   // getCost (KGMT.cu:631-633), as the insert computes it
@@ -1376,6 +1317,34 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) voi
             atomicAdd(valid ? &d.R2Valid[q2] : &d.R2Invalid[q2], 1);
         }
     }
+    {   // tags must read t; a word read before the planner published it is re-read (bounded)
+        const unsigned want = (unsigned)t;
+        bool stale = look && (((unsigned)(sw >> 32) != want) | ((unsigned)(aw >> 32) != want));
+        if (__ballot(stale) != 0ull) {
+            const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
+            for (;;) {
+                __builtin_amdgcn_s_sleep(8);
+                if (stale) {
+                    sw = __hip_atomic_load(pubCur + q1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    aw = __hip_atomic_load(pubCur + d.nR1 + (q2 >> 5), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    stale = ((unsigned)(sw >> 32) != want) | ((unsigned)(aw >> 32) != want);
+                }
+                if (__ballot(stale) == 0ull) break;
+                if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > kStepWaitTicks) {   // give up, report
+                    if (stale) atomicExch(&d.status->error, kErrStepHandoff);
+                    break;
+                }
+            }
+        }
+    }
+    bool accept = false;
+    if (look) {
+        const uint32_t bit = 1u << (q2 & 31);
+        const bool r2Avail = (uint32_t)aw & bit;
+        accept = (u <= __uint_as_float((uint32_t)sw)) || !r2Avail;
+        if (!r2Avail) atomicOr(&sNew[q2 >> 5], bit);
+    }
+    SBMP_STAMP(4);
     const unsigned long long mask = __ballot(accept);
     const unsigned long long word0 =   // lane 0's word
         ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)(word >> 32), 0) << 32) |
@@ -1394,25 +1363,24 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) voi
         const float dx = cs.x - d.goalX, dy = cs.y - d.goalY;   // inGoalRegion, KGMT.cu:635-638
         inGoal = __builtin_sqrtf(dx * dx + dy * dy) < d.goalThreshold;
     }
+    // index among the wave's flagged slots; the first goal child is the wave's lowest
+    const int idxW = __popcll(wordAll & ((1ull << lane) - 1ull));
+    const int glW = first_lane_value(flagged && inGoal, idxW, kNoGoalIdx);
     if (lane == 0) {
         d.gnewOut[slot >> 6] = wordAll;
         sWaveCnt[wave] = __popcll(wordAll);
+        sWaveGoal[wave] = glW;
     }
     __syncthreads();
     SBMP_STAMP(5);
-    int idx = 0;
-    idx += (wave > 0 ? sWaveCnt[0] : 0) + (wave > 1 ? sWaveCnt[1] : 0) + (wave > 2 ? sWaveCnt[2] : 0);
-    const int cntB = sWaveCnt[0] + sWaveCnt[1] + sWaveCnt[2] + sWaveCnt[3];
-    idx += __popcll(wordAll & ((1ull << lane) - 1ull));
+    const int c0 = sWaveCnt[0], c1 = sWaveCnt[1], c2 = sWaveCnt[2], c3 = sWaveCnt[3];
+    const int waveOff = (wave > 0 ? c0 : 0) + (wave > 1 ? c1 : 0) + (wave > 2 ? c2 : 0);
     if (flagged) {
-        float4* e = d.stepList + ((size_t)cp * d.nBlocks * kBlock + (size_t)b * kBlock + idx) * kStepEntry;
+        float4* e = d.stepList + ((size_t)cp * d.nBlocks * kBlock + (size_t)b * kBlock + waveOff + idxW) * kStepEntry;
         e[0] = cs;
         e[1] = cc;
         e[2] = make_float4(cost, 0.0f, 0.0f, 0.0f);
     }
-    // idx grows with the lane: the first goal child is the wave's lowest
-    const int gl = first_lane_value(flagged && inGoal, idx, kNoGoalIdx);
-    if (lane == 0) sRed[1][wave] = gl;
     {   // one 64-bit atomic per touched cell, into this workgroup's replica
         unsigned long long* const rep =
             d.stepDelta + (size_t)(t % 3) * kDeltaReps * d.nR1 + (size_t)(b % kDeltaReps) * d.nR1;
@@ -1420,18 +1388,18 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) voi
         if (v) atomicAdd(&rep[tid], (unsigned long long)(v & 0xffff) | ((unsigned long long)(v >> 16) << 32));
     }
     uint32_t* const newCur = d.stepR2New + (size_t)(t % 3) * nW;
-#pragma unroll
-    for (int j = 0; j < kMaxR2Words / kBlock; ++j) {
-        const int i = tid + j * kBlock;
-        if (j * kBlock < nW && i < nW) {
-            const uint32_t w = sNew[i];
-            if (w) atomicOr(&newCur[i], w);
-        }
+    for (int i = tid; i < nW; i += kBlock) {
+        const uint32_t w = sNew[i];
+        if (w) atomicOr(&newCur[i], w);
     }
-    __syncthreads();
-    if (tid == 0) {
-        const int gmin2 = min(min(sRed[1][0], sRed[1][1]), min(sRed[1][2], sRed[1][3]));
-        d.stepCnt[(size_t)cp * kMaxStepBlocks + b] = cntB | ((gmin2 == kNoGoalIdx ? 0 : gmin2 + 1) << 16);
+    if (tid == 0) {   // the block's flagged count and its lowest goal child (in-block index)
+        const int g0 = sWaveGoal[0], g1 = sWaveGoal[1], g2 = sWaveGoal[2], g3 = sWaveGoal[3];
+        int gmin = kNoGoalIdx;
+        if (g3 != kNoGoalIdx) gmin = c0 + c1 + c2 + g3;
+        if (g2 != kNoGoalIdx) gmin = c0 + c1 + g2;
+        if (g1 != kNoGoalIdx) gmin = c0 + g1;
+        if (g0 != kNoGoalIdx) gmin = g0;
+        d.stepCnt[(size_t)cp * kMaxStepBlocks + b] = (c0 + c1 + c2 + c3) | ((gmin == kNoGoalIdx ? 0 : gmin + 1) << 16);
     }
     SBMP_STAMP(6);
     if (tl) {
