@@ -183,6 +183,7 @@ struct KgmtDev {
     long long* timeline;
     long long* timelineFin;   // k_finish(timelineIter): [1 + nBlocks][kTimelineStamps], wave 0 of each workgroup
     int timelineIter;
+    int obsNaN;   // a register-held obstacle has a NaN coordinate: wave_cull keeps every box
 };
 
 // 16-B / 8-B stores with sc1: written through to memory during the kernel, so the
@@ -270,6 +271,40 @@ __device__ __forceinline__ int getR2_k(float x, float y, int r1, float R1Size, i
     const int cx = cell_of(div_or_ieee(lx, R2Size, rcpR2), &okx);
     const int cy = cell_of(div_or_ieee(ly, R2Size, rcpR2), &oky);
     return (okx && oky && cx >= 0 && cx < n && cy >= 0 && cy < n) ? r1 * (n * n) + cy * n + cx : -1;
+}
+
+// getR1 and getR2 of one state in one pass (what getR1_k then getR2_k return).  The
+// range tests of cell_of and of getR1 / getR2 fold into one pair of comparisons per
+// axis: cell_of(q) is defined and in [0, N) iff -1 < q < N (the conversion truncates
+// toward zero; a NaN fails both), and the R1 cell's (cx, cy) are the ones getR2
+// re-derives from r1.  One uniform branch picks the reciprocal or the IEEE quotients.
+__device__ __forceinline__ void bins_k(float x, float y, const KgmtDev& d, int* r1, int* r2) {
+    float qx, qy;
+    const bool fast = (d.rcpR1Size != 0.0f) & (d.rcpR2Size != 0.0f);
+    if (fast) {
+        qx = div_by(x, d.R1Size, d.rcpR1Size);
+        qy = div_by(y, d.R1Size, d.rcpR1Size);
+    } else {
+        qx = x / d.R1Size;
+        qy = y / d.R1Size;
+    }
+    const float fN = (float)kN, fn = (float)d.n;
+    const bool in1 = (qx > -1.0f) & (qx < fN) & (qy > -1.0f) & (qy < fN);
+    const int cx = in1 ? (int)qx : 0, cy = in1 ? (int)qy : 0;
+    const float lx = __builtin_fmaf(-(float)cx, d.R1Size, x);   // nvcc's contraction of KGMT.cu:620 (D10)
+    const float ly = __builtin_fmaf(-(float)cy, d.R1Size, y);
+    float px, py;
+    if (fast) {
+        px = div_by(lx, d.R2Size, d.rcpR2Size);
+        py = div_by(ly, d.R2Size, d.rcpR2Size);
+    } else {
+        px = lx / d.R2Size;
+        py = ly / d.R2Size;
+    }
+    const bool in2 = in1 & (px > -1.0f) & (px < fn) & (py > -1.0f) & (py < fn);
+    const int c = cy * kN + cx;
+    *r1 = in1 ? c : -1;
+    *r2 = in2 ? (c * d.n + (int)py) * d.n + (int)px : -1;
 }
 
 // ---------------------------------------------------------------- cuRAND XORWOW
@@ -418,19 +453,36 @@ struct WaveCull {
     bool bounds;       // some lane may leave the workspace (wave-uniform)
 };
 
+// The square test as vector arithmetic: a box (minx, miny)-(maxx, maxy) meets obstacle
+// o under isBroadPhaseValid's predicate iff max(o.x - maxx, minx - o.z, o.y - maxy,
+// miny - o.w) < 0 (for finite operands a - b < 0 <=> a < b exactly: IEEE subtraction
+// with gradual underflow, .amdhsa_float_denorm_mode_32 3).  maxnum ignores a NaN
+// operand, so a list with a NaN coordinate keeps every box (KgmtDev::obsNaN).
+__device__ __forceinline__ float vmax3(float a, float b, float c) { return __builtin_fmaxf(__builtin_fmaxf(a, b), c); }
+__device__ __forceinline__ float vmin3(float a, float b, float c) { return __builtin_fminf(__builtin_fminf(a, b), c); }
+
 template <int OBS>
 __device__ __forceinline__ WaveCull wave_cull(float x0, float y0, float rx, float ry, const float4* obs,
                                               const KgmtDev& d) {
     WaveCull w;
     rx = rx * 1.0001f + 1e-3f;
     ry = ry * 1.0001f + 1e-3f;
-    const float minx = x0 - rx, maxx = x0 + rx, miny = y0 - ry, maxy = y0 + ry;
-    const bool inside = (minx > 0.0f) & (maxx < d.width) & (miny > 0.0f) & (maxy < d.height);
+    const sbmp_f32x2 c = {x0, y0}, rr = {rx, ry};
+    const sbmp_f32x2 mn = c - rr, mx = c + rr;
+    const sbmp_f32x2 far = sbmp_f32x2{d.width, d.height} - mx;
+    // (minx > 0) & (maxx < W) & (miny > 0) & (maxy < H), as min(...) > 0 (see above)
+    const bool inside = __builtin_fminf(vmin3(mn.x, mn.y, far.x), far.y) > 0.0f;
     w.bounds = __ballot(!inside) != 0ull;
     w.boxes = 0u;
 #pragma unroll
-    for (int i = 0; i < obs_in_registers(OBS); ++i)
-        if (__ballot(box_overlap(minx, miny, maxx, maxy, obs[i])) != 0ull) w.boxes |= 1u << i;
+    for (int i = 0; i < obs_in_registers(OBS); ++i) {
+        const float4 o = obs[i];
+        const sbmp_f32x2 lo = sbmp_f32x2{o.x, o.y} - mx;
+        const sbmp_f32x2 hi = mn - sbmp_f32x2{o.z, o.w};
+        const float sep = __builtin_fmaxf(vmax3(lo.x, lo.y, hi.x), hi.y);
+        if (__ballot(sep < 0.0f) != 0ull) w.boxes |= 1u << i;
+    }
+    if (d.obsNaN) w.boxes = ~0u;
     return w;
 }
 
@@ -597,6 +649,94 @@ __device__ __forceinline__ bool point_euler(float4 p, const ChildCtl& ctl, const
     out.steer = vy;
     out.dur = duration;
     return alive;
+}
+
+// ---------------------------------------------------------------- fast car loop
+// The Euler loop of a car child for register obstacle lists, written for k_step's
+// budget of vector AND scalar instructions (both ran near their limits: 1,141 VALU
+// and 875 SALU per wave, 16 waves per CU sharing one scalar unit):
+//   - no per-lane branches: a lane whose child ended keeps its state by selects, as
+//     at the reference's break (statePropagator.cu:42-45, 61-64), so no exec-mask
+//     save / restore / merge per step;
+//   - the workspace test (statePropagator.cu:42-45) as min(x, y, W - x, H - y) > 0;
+//   - isBroadPhaseValid (collisionCheck.cu:6-14) as the separation metric of wave_cull
+//     (exact for finite operands; a NaN box list never takes this loop), one uniform
+//     branch per box the wave's cull kept, the metric a float (no lane-mask merge);
+//   - sincos on its Cody-Waite branch only: car_fast_ok admits a wave only if every
+//     lane's theta provably stays below 1e5 (|theta| <= |theta0| + T (|v0| + |a| T) |tan| / L).
+// The results are those of car_euler bit for bit (the same operations on the same
+// values; the tests only replace comparisons by exact equivalents).
+
+// min(a, b, c, e) without the canonicalising v_max that minnum adds in IEEE mode for
+// operands the compiler cannot prove canonical (packed-FMA results).
+__device__ __forceinline__ float min4_asm(float a, float b, float c, float e) {
+    float r;
+    asm("v_min3_f32 %0, %1, %2, %3\n\tv_min_f32 %0, %0, %4" : "=&v"(r) : "v"(a), "v"(b), "v"(c), "v"(e));
+    return r;
+}
+
+// >= 0: the box (mn, mx) is separated from obstacle o (wave_cull's metric).
+__device__ __forceinline__ float box_sep(sbmp_f32x2 mn, sbmp_f32x2 mx, float4 o) {
+    const sbmp_f32x2 lo = sbmp_f32x2{o.x, o.y} - mx;
+    const sbmp_f32x2 hi = mn - sbmp_f32x2{o.z, o.w};
+    return __builtin_fmaxf(vmax3(lo.x, lo.y, hi.x), hi.y);
+}
+
+// true if this wave may take car_euler_fast: L a power of two (v / L is one multiply),
+// no NaN box, and theta below the Cody-Waite range on every lane for every step.
+__device__ __forceinline__ bool car_fast_ok(float4 p, const ChildCtl& c, const KgmtDev& d) {
+    const float T = c.dur;
+    const float bound = __builtin_fabsf(p.z) + T * (__builtin_fabsf(p.w) + __builtin_fabsf(c.a) * T) *
+                                                   __builtin_fabsf(c.tanS) * __builtin_fabsf(d.invAgentLength) * 1.01f;
+    return __ballot(!(bound <= 1.0e5f)) == 0ull && d.invAgentLength != 0.0f && !d.obsNaN;
+}
+
+template <int OBS>
+__device__ __forceinline__ bool car_euler_fast(float4 p, const ChildCtl& ctl, const KgmtDev& d, const float4* obs,
+                                               ChildOut& out) {
+    constexpr int NOBS = obs_in_registers(OBS);
+    const float a = ctl.a, T = ctl.dur, dt = ctl.dt;
+    sbmp_f32x2 xy = {p.x, p.y}, tv = {p.z, p.w};
+    const sbmp_f32x2 dt2 = {dt, dt}, wh = {d.width, d.height};
+    const float invL = d.invAgentLength;
+    const float r = T * __builtin_fabsf(p.w) + 0.5f * __builtin_fabsf(a) * T * T;
+    const WaveCull cull = wave_cull<OBS>(p.x, p.y, r, r, obs, d);
+    float aliveF = 1.0f;   // 1 alive, 0 ended: a float, so no lane mask is carried across steps
+    for (int i = 0; i < d.numDisc; ++i) {
+        const float x = tv.x;   // sincos_pred, Cody-Waite branch
+        const float j = __builtin_rintf(x * 0.636619772f);
+        float rr = __builtin_fmaf(j, -1.57079601e+00f, x);
+        rr = __builtin_fmaf(j, -3.13916473e-07f, rr);
+        rr = __builtin_fmaf(j, -5.39030253e-15f, rr);
+        float st, ct;
+        sincos_quadrant(rr, (int)j, &st, &ct);
+        const sbmp_f32x2 nxy = __builtin_elementwise_fma(sbmp_f32x2{tv.y, tv.y} * sbmp_f32x2{ct, st}, dt2, xy);
+        const sbmp_f32x2 far = wh - nxy;   // W - x, H - y
+        const float vl = tv.y * invL;     // v / L, exact for a power-of-two L
+        const sbmp_f32x2 ntv = __builtin_elementwise_fma(sbmp_f32x2{vl * ctl.tanS, a}, dt2, tv);
+        float sep = 1.0f;   // >= 0: free of every kept box
+        if (cull.boxes) {
+            const sbmp_f32x2 mn = {seg_min(xy.x, nxy.x), seg_min(xy.y, nxy.y)};
+            const sbmp_f32x2 mx = {seg_max(xy.x, nxy.x), seg_max(xy.y, nxy.y)};
+#pragma unroll
+            for (int k = 0; k < NOBS; ++k)
+                if ((cull.boxes >> k) & 1u) sep = __builtin_fminf(sep, box_sep(mn, mx, obs[k]));   // uniform branch
+        }
+        // the reference's break: out of bounds keeps the new (x, y) and the old
+        // (theta, v); a collision keeps all four
+        const bool live = aliveF > 0.0f;
+        const float in4 = cull.bounds ? min4_asm(aliveF, nxy.x, nxy.y, __builtin_fminf(far.x, far.y)) : aliveF;
+        const bool upd = in4 > 0.0f;   // alive & inside
+        xy = live ? nxy : xy;
+        tv = upd ? ntv : tv;
+        aliveF = (upd & (sep >= 0.0f)) ? 1.0f : 0.0f;
+    }
+    asm volatile("" : "+v"(aliveF));   // keep the last step's masks from living across the loop
+    out.state = make_float4(xy.x, xy.y, tv.x, tv.y);
+    out.a = a;
+    out.steer = ctl.steer;
+    out.dur = T;
+    return aliveF > 0.0f;
 }
 
 // reference statePropagator.cu:5-76: controls, then the Euler loop (k_expand's form).

@@ -1279,15 +1279,19 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) voi
     const float4* obs = (kRegObs > 0) ? ro : kLdsObs ? sObs : d.obstacles;
     ChildOut out;
     bool valid = false;
-    if (act) valid = (AGENT == 0) ? car_euler<OBS>(p, ctl, d, obs, out) : point_euler<OBS>(p, ctl, d, obs, out);
+    // The fast loop runs on every lane, outside any divergent branch, so its lane masks
+    // need no merging with exec: inactive lanes (slots >= S) propagate row 0 with
+    // controls from their unused stream, and their result is dropped.
+    if (AGENT == 0 && kRegObs > 0 && car_fast_ok(p, ctl, d)) {   // the common case (wave-uniform)
+        valid = car_euler_fast<OBS>(p, ctl, d, obs, out) && act;
+    } else if (act) {
+        valid = (AGENT == 0) ? car_euler<OBS>(p, ctl, d, obs, out) : point_euler<OBS>(p, ctl, d, obs, out);
+    }
     SBMP_STAMP(3);
 
     // ---- bins (KGMT.cu:390-391) and the accept test (KGMT.cu:394-411, D2)
     int q1 = -1, q2 = -1;
-    if (act) {
-        q1 = getR1_k(out.state.x, out.state.y, d.R1Size, d.rcpR1Size, kN);   // N = 16 (KGMT.cu:8)
-        q2 = getR2_k(out.state.x, out.state.y, q1, d.R1Size, kN, d.R2Size, d.rcpR2Size, d.n);
-    }
+    if (act) bins_k(out.state.x, out.state.y, d, &q1, &q2);   // N = 16 (KGMT.cu:8)
     // The planner workgroup publishes iteration t's scores and snapshot as 8-B words
     // tagged with t (step_planner); each lane that takes the test reads its two words
     // from L2 now, and the stores below overlap that round trip.  q2 >= 0 implies q1 >= 0.

@@ -359,6 +359,14 @@ void KgmtPlanner::begin(const float* initial, const float* goal, const float* d_
         SBMP_HIP(hipMemcpyAsync(obs_, d_obstacles, sizeof(float4) * nObs, hipMemcpyDeviceToDevice, s));
     d.obstacles = obs_;
     d.nObs = nObs;
+    d.obsNaN = 0;
+    if (nObs > 0 && nObs <= kMaxRegObs) {   // register lists: wave_cull's separation metric ignores NaN
+        float h[4 * kMaxRegObs];
+        SBMP_HIP(hipMemcpyAsync(h, d_obstacles, sizeof(float) * 4 * nObs, hipMemcpyDeviceToHost, s));
+        SBMP_HIP(hipStreamSynchronize(s));
+        for (int i = 0; i < 4 * nObs; ++i)
+            if (std::isnan(h[i])) d.obsNaN = 1;
+    }
     // Large obstacle lists: the uniform-grid index (include/sbmp/obstacle_grid.h),
     // built on the host from the caller's boxes; the global all-boxes loop remains
     // as variant 5.

@@ -1,5 +1,9 @@
-"""GPU parity at the benchmark configurations (BASELINE.json configs c2-c5), whole state
+"""GPU parity at the benchmark configurations (BASELINE.json configs c1-c5), whole state
 bit-exact against the CPU oracle -- not properties.
+
+  c1  exactly as systems/c1.yaml states it: the R2 point agent, 1,024 samples per
+      iteration, M = 2^20, fill rule, complete GNew clear, 100 iterations, read through
+      the library's config parser (sbmp_load_system_config).
 
   c3  the exact bench mode: car, S = 262,144/iteration, M = 2^24, fill rule (D14),
       complete GNew clear, seed 20240807, 72 iterations: covers the driver's timed
@@ -50,6 +54,23 @@ def _bench_kw(S, iters, **kw):
 def _c5_obstacles():
     from cudasbmp_amd import read_obstacles_csv
     return read_obstacles_csv(os.path.join(ROOT, "configurations", "obstacles", "obstacles_c5.csv"))
+
+
+def test_c1_as_configured_bit_exact(oracle_lib):
+    from cudasbmp_amd import KGMT, DeviceBuffer, read_obstacles_csv
+    from cudasbmp_amd.config import workload
+    cfg = workload("c1")
+    assert cfg["agent"] == "point" and cfg["samplesPerIteration"] == 1024 and cfg["batchRule"] == "fill"
+    obs = read_obstacles_csv(cfg["obstacles"])
+    pl = dict(cfg["planner"])
+    extra = dict(samplesPerIteration=1024, agent="point", batchRule="fill", fixGNewClear=True)
+    g = KGMT(**pl, **extra)
+    r = g.plan(cfg["initial"], cfg["goal"], DeviceBuffer(obs), len(obs), seed=BENCH_SEED)
+    o = _oracle(pl, extra)
+    o.plan(cfg["initial"], cfg["goal"], obs, BENCH_SEED)
+    assert r.iterations == pl["numIterations"] == 100
+    assert g.iter_log()[:, 5].max() == 1024   # fill rule: S = k * nExp <= 1024 (D14)
+    assert_same_state(g, o, label="c1 as configured")
 
 
 def test_c3_bench_mode_bit_exact(obstacles, oracle_lib):

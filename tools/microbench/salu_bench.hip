@@ -1,6 +1,6 @@
-// SALU issue rate per CU: 8 independent s_mul_i32 chains per wave (s_mul_i32 leaves SCC
+// SALU issue rate per CU: 8 independent s_add_u32 chains per wave (each asm declares its SCC write,
 // alone, so the loop's own compare survives the asm), at 1..4 waves per SIMD (4..16 per
-// CU); and SALU + VALU interleaved (one s_mul_i32 per v_fma_f32) to see whether the
+// CU); and SALU + VALU interleaved (one s_add_u32 per v_fma_f32) to see whether the
 // scalar unit issues beside the vector units.  Answers how much of k_step's ~875 SALU per
 // wave (16 waves per CU) is a serial cost of its own.
 //   hipcc -O3 --offload-arch=gfx950 tools/microbench/salu_bench.hip -o tools/microbench/salu_bench
@@ -16,7 +16,7 @@ __global__ __launch_bounds__(256) void k_salu(float* out, int iters, int seed) {
     for (int i = 0; i < 8; ++i) a[i] = threadIdx.x * 1e-3f + i;
     const float b = 0.999f, c = 1e-4f;
     for (int it = 0; it < iters; ++it) {
-#define SM(x) asm volatile("s_mul_i32 %0, %0, 3" : "+s"(x))
+#define SM(x) asm volatile("s_add_u32 %0, %0, 3" : "+s"(x) : : "scc")
 #define VF(i) asm volatile("v_fma_f32 %0, %0, %1, %2" : "+v"(a[i]) : "v"(b), "v"(c))
         SM(s0); if (MIX) VF(0);
         SM(s1); if (MIX) VF(1);
@@ -56,7 +56,7 @@ int main() {
             }
             const double perCu = (double)iters * 8 * 4 * w;   // SALU instructions per CU
             printf("%-26s waves/CU %2d: %.3f ms, %.3f ns per SALU instr per CU%s\n",
-                   mix ? "s_mul_i32 + v_fma_f32" : "s_mul_i32", 4 * w, ms, ms * 1e6 / perCu,
+                   mix ? "s_add_u32 + v_fma_f32" : "s_add_u32", 4 * w, ms, ms * 1e6 / perCu,
                    mix ? " (one v_fma_f32 per SALU instr)" : "");
         }
     }
