@@ -411,12 +411,32 @@ __device__ __forceinline__ void sincos_quadrant(float r, int q, float* s, float*
     *c = u2f(f2u(c0) ^ ((uint32_t)((q + 1) & 2) << 30));
 }
 
-__device__ __forceinline__ void sincos_pred(float x, float* s, float* c) {
+// sincos_pred's Cody-Waite branch with the same operations (hence bits) as
+// sincos_quadrant(sincos_poly2): the polynomial pairs packed, the last two FMAs scalar
+// (the packed form needed two register copies to pair its operands).
+__device__ __forceinline__ void sincos_cw(float x, float* s, float* c) {
     const float j = __builtin_rintf(x * 0.636619772f);
     float r = __builtin_fmaf(j, -1.57079601e+00f, x);
     r = __builtin_fmaf(j, -3.13916473e-07f, r);
     r = __builtin_fmaf(j, -5.39030253e-15f, r);
-    sincos_quadrant(r, (int)j, s, c);
+    const int q = (int)j;
+    const float z = r * r;
+    const sbmp_f32x2 zz = {z, z};
+    sbmp_f32x2 p = __builtin_elementwise_fma(sbmp_f32x2{-1.9515295891e-4f, 2.443315711809948e-5f}, zz,
+                                             sbmp_f32x2{8.3321608736e-3f, -1.388731625493765e-3f});
+    p = __builtin_elementwise_fma(p, zz, sbmp_f32x2{-1.6666654611e-1f, 4.166664568298827e-2f});
+    const sbmp_f32x2 pz = p * zz;
+    const float sp = __builtin_fmaf(pz.x, r, r);
+    const float cp = __builtin_fmaf(pz.y, z, __builtin_fmaf(-0.5f, z, 1.0f));
+    const bool odd = (q & 1) != 0;
+    const float s0 = odd ? cp : sp;
+    const float c0 = odd ? sp : cp;
+    *s = u2f(f2u(s0) ^ ((uint32_t)(q & 2) << 30));
+    *c = u2f(f2u(c0) ^ ((uint32_t)((q + 1) & 2) << 30));
+}
+
+__device__ __forceinline__ void sincos_pred(float x, float* s, float* c) {
+    sincos_cw(x, s, c);
     if (!(__builtin_fabsf(x) <= 105615.0f)) {   // rare: huge, inf or NaN argument
         if (finitef(x)) {
             int q;
@@ -662,8 +682,8 @@ __device__ __forceinline__ bool point_euler(float4 p, const ChildCtl& ctl, const
 //   - isBroadPhaseValid (collisionCheck.cu:6-14) as the separation metric of wave_cull
 //     (exact for finite operands; a NaN box list never takes this loop), one uniform
 //     branch per box the wave's cull kept, the metric a float (no lane-mask merge);
-//   - sincos on its Cody-Waite branch only: car_fast_ok admits a wave only if every
-//     lane's theta provably stays below 1e5 (|theta| <= |theta0| + T (|v0| + |a| T) |tan| / L).
+//   - sincos_pred: Cody-Waite on every lane, Payne-Hanek only for a lane past 105615
+//     (a steering angle near +-pi/2 makes theta grow that far within a child).
 // The results are those of car_euler bit for bit (the same operations on the same
 // values; the tests only replace comparisons by exact equivalents).
 
@@ -682,45 +702,40 @@ __device__ __forceinline__ float box_sep(sbmp_f32x2 mn, sbmp_f32x2 mx, float4 o)
     return __builtin_fmaxf(vmax3(lo.x, lo.y, hi.x), hi.y);
 }
 
-// true if this wave may take car_euler_fast: L a power of two (v / L is one multiply),
-// no NaN box, and theta below the Cody-Waite range on every lane for every step.
-__device__ __forceinline__ bool car_fast_ok(float4 p, const ChildCtl& c, const KgmtDev& d) {
-    const float T = c.dur;
-    const float bound = __builtin_fabsf(p.z) + T * (__builtin_fabsf(p.w) + __builtin_fabsf(c.a) * T) *
-                                                   __builtin_fabsf(c.tanS) * __builtin_fabsf(d.invAgentLength) * 1.01f;
-    return __ballot(!(bound <= 1.0e5f)) == 0ull && d.invAgentLength != 0.0f && !d.obsNaN;
-}
+// true if this wave may take car_euler_fast: L a power of two (v / L is one multiply)
+// and no NaN box (the separation metric ignores NaN).  Per plan, so wave-uniform.
+__device__ __forceinline__ bool car_fast_ok(const KgmtDev& d) { return d.invAgentLength != 0.0f && !d.obsNaN; }
 
 template <int OBS>
 __device__ __forceinline__ bool car_euler_fast(float4 p, const ChildCtl& ctl, const KgmtDev& d, const float4* obs,
                                                ChildOut& out) {
     constexpr int NOBS = obs_in_registers(OBS);
     const float a = ctl.a, T = ctl.dur, dt = ctl.dt;
-    sbmp_f32x2 xy = {p.x, p.y}, tv = {p.z, p.w};
+    // (v, theta): v in the low half, so the packed products broadcast it without a copy
+    sbmp_f32x2 xy = {p.x, p.y}, vt = {p.w, p.z};
     const sbmp_f32x2 dt2 = {dt, dt}, wh = {d.width, d.height};
     const float invL = d.invAgentLength;
     const float r = T * __builtin_fabsf(p.w) + 0.5f * __builtin_fabsf(a) * T * T;
     const WaveCull cull = wave_cull<OBS>(p.x, p.y, r, r, obs, d);
+    unsigned kept = __builtin_amdgcn_readfirstlane(cull.boxes);   // wave-uniform (a ballot)
     float aliveF = 1.0f;   // 1 alive, 0 ended: a float, so no lane mask is carried across steps
     for (int i = 0; i < d.numDisc; ++i) {
-        const float x = tv.x;   // sincos_pred, Cody-Waite branch
-        const float j = __builtin_rintf(x * 0.636619772f);
-        float rr = __builtin_fmaf(j, -1.57079601e+00f, x);
-        rr = __builtin_fmaf(j, -3.13916473e-07f, rr);
-        rr = __builtin_fmaf(j, -5.39030253e-15f, rr);
+        // re-tested every step (s_bitcmp1 + branch): hoisted, each kept flag would hold
+        // a 64-bit lane mask in scalar registers for the whole loop
+        if (NOBS > 1) asm volatile("" : "+s"(kept));   // (one box: a single flag either way)
         float st, ct;
-        sincos_quadrant(rr, (int)j, &st, &ct);
-        const sbmp_f32x2 nxy = __builtin_elementwise_fma(sbmp_f32x2{tv.y, tv.y} * sbmp_f32x2{ct, st}, dt2, xy);
+        sincos_pred(vt.y, &st, &ct);   // Payne-Hanek for the rare lane past 105615 (a huge steering tan)
+        const sbmp_f32x2 nxy = __builtin_elementwise_fma(sbmp_f32x2{vt.x, vt.x} * sbmp_f32x2{ct, st}, dt2, xy);
         const sbmp_f32x2 far = wh - nxy;   // W - x, H - y
-        const float vl = tv.y * invL;     // v / L, exact for a power-of-two L
-        const sbmp_f32x2 ntv = __builtin_elementwise_fma(sbmp_f32x2{vl * ctl.tanS, a}, dt2, tv);
+        const float vl = vt.x * invL;     // v / L, exact for a power-of-two L
+        const sbmp_f32x2 nvt = __builtin_elementwise_fma(sbmp_f32x2{a, vl * ctl.tanS}, dt2, vt);
         float sep = 1.0f;   // >= 0: free of every kept box
-        if (cull.boxes) {
+        if (kept) {
             const sbmp_f32x2 mn = {seg_min(xy.x, nxy.x), seg_min(xy.y, nxy.y)};
             const sbmp_f32x2 mx = {seg_max(xy.x, nxy.x), seg_max(xy.y, nxy.y)};
 #pragma unroll
             for (int k = 0; k < NOBS; ++k)
-                if ((cull.boxes >> k) & 1u) sep = __builtin_fminf(sep, box_sep(mn, mx, obs[k]));   // uniform branch
+                if ((kept >> k) & 1u) sep = seg_min(sep, box_sep(mn, mx, obs[k]));   // uniform branch
         }
         // the reference's break: out of bounds keeps the new (x, y) and the old
         // (theta, v); a collision keeps all four
@@ -728,11 +743,11 @@ __device__ __forceinline__ bool car_euler_fast(float4 p, const ChildCtl& ctl, co
         const float in4 = cull.bounds ? min4_asm(aliveF, nxy.x, nxy.y, __builtin_fminf(far.x, far.y)) : aliveF;
         const bool upd = in4 > 0.0f;   // alive & inside
         xy = live ? nxy : xy;
-        tv = upd ? ntv : tv;
+        vt = upd ? nvt : vt;
         aliveF = (upd & (sep >= 0.0f)) ? 1.0f : 0.0f;
     }
     asm volatile("" : "+v"(aliveF));   // keep the last step's masks from living across the loop
-    out.state = make_float4(xy.x, xy.y, tv.x, tv.y);
+    out.state = make_float4(xy.x, xy.y, vt.y, vt.x);
     out.a = a;
     out.steer = ctl.steer;
     out.dur = T;

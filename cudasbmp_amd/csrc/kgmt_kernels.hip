@@ -1282,11 +1282,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) voi
     // The fast loop runs on every lane, outside any divergent branch, so its lane masks
     // need no merging with exec: inactive lanes (slots >= S) propagate row 0 with
     // controls from their unused stream, and their result is dropped.
-    if (AGENT == 0 && kRegObs > 0 && car_fast_ok(p, ctl, d)) {   // the common case (wave-uniform)
-        valid = car_euler_fast<OBS>(p, ctl, d, obs, out) && act;
-    } else if (act) {
-        valid = (AGENT == 0) ? car_euler<OBS>(p, ctl, d, obs, out) : point_euler<OBS>(p, ctl, d, obs, out);
+    bool fast = false;
+    if constexpr (AGENT == 0 && kRegObs > 0) {
+        fast = car_fast_ok(d);   // per plan (uniform)
+        if (fast) valid = car_euler_fast<OBS>(p, ctl, d, obs, out) && act;
     }
+    if (!fast && act)
+        valid = (AGENT == 0) ? car_euler<OBS>(p, ctl, d, obs, out) : point_euler<OBS>(p, ctl, d, obs, out);
     SBMP_STAMP(3);
 
     // ---- bins (KGMT.cu:390-391) and the accept test (KGMT.cu:394-411, D2)

@@ -82,16 +82,23 @@ SBMP_HD float reduce_payne_hanek(float x, int* q_out) {
     Q[SBMP_TWO_OVER_PI_WORDS] = (uint32_t)carry;
     // x*2/pi = Q * 2^(E-255): the binary point sits at bit p = 255 - E.
     // Take the 64-bit window W = Q[p-62 .. p+1]: 2 integer bits + 62 fraction bits.
+    // 16 <= E <= 127 (|x| >= 2^16, finite), so lo_bit is in [66, 177] and the window
+    // starts in word 2..5: three 4-way selects, then two 32-bit funnel shifts
+    // (v_alignbit_b32 on the device).  The same bits as shifting the whole of Q.
     const int lo_bit = 255 - E - 62;
     const int wi = lo_bit >> 5;
     const int sh = lo_bit & 31;
-    const uint64_t w0 = Q[wi], w1 = Q[wi + 1], w2 = Q[wi + 2];
-    uint64_t W;
-    if (sh == 0) {
-        W = w0 | (w1 << 32);
-    } else {
-        W = (w0 >> sh) | (w1 << (32 - sh)) | (w2 << (64 - sh));
-    }
+    const uint32_t w0 = wi <= 2 ? Q[2] : wi == 3 ? Q[3] : wi == 4 ? Q[4] : Q[5];
+    const uint32_t w1 = wi <= 2 ? Q[3] : wi == 3 ? Q[4] : wi == 4 ? Q[5] : Q[6];
+    const uint32_t w2 = wi <= 2 ? Q[4] : wi == 3 ? Q[5] : wi == 4 ? Q[6] : Q[7];
+#if defined(__HIP_DEVICE_COMPILE__)
+    const uint32_t lo = __builtin_amdgcn_alignbit(w1, w0, (uint32_t)sh);
+    const uint32_t hi = __builtin_amdgcn_alignbit(w2, w1, (uint32_t)sh);
+#else
+    const uint32_t lo = (uint32_t)((((uint64_t)w1 << 32) | w0) >> sh);
+    const uint32_t hi = (uint32_t)((((uint64_t)w2 << 32) | w1) >> sh);
+#endif
+    const uint64_t W = ((uint64_t)hi << 32) | lo;
     int q = (int)(W >> 62);
     int64_t f = (int64_t)(W & 0x3fffffffffffffffull);     // fraction in 0.62 fixed point
     if (f >= (int64_t)0x2000000000000000ll) {              // fraction >= 1/2: round quadrant up

@@ -4,4 +4,3 @@ timeout -k 10 500 python3 -u -m pytest tests -x -q -m gpu --timeout 120 --timeou
 tail -1 gpurun_out/r03/gpu_tests.log
 bash tools/ab_drv.sh 3 prev=_ab/prev new=. || exit 1
 bash tools/pmc_sq.sh gpurun_out/r03/pmc_new || exit 1
-(cd _ab/prev && bash tools/pmc_sq.sh ../../gpurun_out/r03/pmc_prev) || exit 1
