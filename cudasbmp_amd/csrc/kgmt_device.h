@@ -85,6 +85,7 @@ constexpr uint16_t kNoKey = 0xffff;  // child outside the R2 grid (D3)
 // table serialise there and back up the stores of the CUs behind them (k_expand
 // 18.7 -> 14.6 us at 8 replicas).
 constexpr int kDeltaReps = 8;
+constexpr int kNewReps = 8;     // k_step R2New replicas (merged by the next planner)
 constexpr int kMaxStepBlocks = 1024;   // k_step: one int4 of block counts per thread (<= 262,144 slots)
 constexpr int kNoGoalIdx = 0x7fffffff;
 constexpr int kFastDivMax = 1 << 24;   // slot counts up to this use the float-estimate division
@@ -162,7 +163,7 @@ struct KgmtDev {
                           // in-block index of a flagged child in the goal region, 0 if none) << 16
     float4* stepList;     // [2][nBlocks * kBlock][kStepEntry] flagged children compacted per block
     unsigned long long* stepDelta;   // [3][kDeltaReps * nR1] packed R1 deltas
-    uint32_t* stepR2New;  // [3][nR2 / 32] R2New bits
+    uint32_t* stepR2New;  // [3][kNewReps][nR2 / 32] R2New bits, replica b % kNewReps per block
     unsigned long long* stepPub;     // [2][nR1 + nR2 / 32] scores and snapshot words, each tagged with t
     uint32_t* R2Snap;     // availability bits at the iteration start (D2)
     int* R2Valid;
@@ -184,6 +185,10 @@ struct KgmtDev {
     long long* timelineFin;   // k_finish(timelineIter): [1 + nBlocks][kTimelineStamps], wave 0 of each workgroup
     int timelineIter;
     int obsNaN;   // a register-held obstacle has a NaN coordinate: wave_cull keeps every box
+    // k_step reads this struct from device memory (a copy the host refreshes before a
+    // launch when it changed): as a 600-B kernel argument its fields were loaded at
+    // entry, spilled to VGPR lanes and reloaded, four serial scalar round trips
+    const KgmtDev* devSelf;
 };
 
 // 16-B / 8-B stores with sc1: written through to memory during the kernel, so the

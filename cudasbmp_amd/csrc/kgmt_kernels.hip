@@ -852,6 +852,14 @@ size_t oneshot_inbox_words(long long n, int nranks) { return (size_t)2 * nranks 
 //   treeSize(t-1) + prefix + index) and applies the D6 clear to its words.
 // expand == 0 is the flush pass run before a read-back (no expansion; the same
 // values are rewritten by k_step(t) proper, so it is idempotent).
+// OR of word w over the kNewReps R2New replicas ([rep][nW] layout: one line per replica)
+__device__ __forceinline__ uint32_t merge_new(const uint32_t* p, int nW, int w) {
+    uint32_t v = 0u;
+#pragma unroll
+    for (int r = 0; r < kNewReps; ++r) v |= p[(size_t)r * nW + w];
+    return v;
+}
+
 __device__ __forceinline__ void step_unpack(int v, int* cnt, int* goal) {
     *cnt = v & 0xffff;
     *goal = (v >> 16) - 1;
@@ -960,13 +968,23 @@ __device__ __forceinline__ void step_planner(const KgmtDev& d, int t, int expand
 #pragma unroll
     for (int r = 0; r < kDeltaReps; ++r) dl += deltaPrev[(size_t)r * d.nR1 + cell];
     const uint32_t* availPrev = d.R2Avail + (size_t)pp * nW;
-    const uint32_t* newPrev = d.stepR2New + (size_t)((t - 1) % 3) * nW;
+    const uint32_t* newPrev = d.stepR2New + (size_t)((t - 1) % 3) * kNewReps * nW;
     uint32_t availW[kW], newW[kW];
 #pragma unroll
     for (int j = 0; j < kW; ++j) {
         const int w = min(tid + j * kBlock, nW - 1);
         availW[j] = availPrev[w];
-        newW[j] = newPrev[w];
+        newW[j] = 0u;
+    }
+    // the R2New replicas: n <= 8 (two words per thread) with all 16 loads in flight;
+    // larger grids one word at a time (8 VGPRs live: all 64 at once would spill)
+    if (nW <= 2 * kBlock) {
+        newW[0] = merge_new(newPrev, nW, min(tid, nW - 1));
+        newW[1] = merge_new(newPrev, nW, min(tid + kBlock, nW - 1));
+    } else {
+#pragma unroll
+        for (int j = 0; j < kW; ++j)
+            if (j * kBlock < nW) newW[j] = merge_new(newPrev, nW, min(tid + j * kBlock, nW - 1));
     }
     for (int i = tid; i < d.nR1; i += kBlock) sCovInc[i] = 0;
     int A, jGoal;
@@ -1065,8 +1083,8 @@ __device__ __forceinline__ void step_planner(const KgmtDev& d, int t, int expand
     {   // ring (t+1) % 3, last read by k_step(t-1): zero for k_step(t+1)
         unsigned long long* zd = d.stepDelta + (size_t)((t + 1) % 3) * kDeltaReps * d.nR1;
         for (int i = tid; i < kDeltaReps * d.nR1; i += kBlock) zd[i] = 0ull;
-        uint32_t* zn = d.stepR2New + (size_t)((t + 1) % 3) * nW;
-        for (int i = tid; i < nW; i += kBlock) zn[i] = 0u;
+        uint32_t* zn = d.stepR2New + (size_t)((t + 1) % 3) * kNewReps * nW;
+        for (int i = tid; i < kNewReps * nW; i += kBlock) zn[i] = 0u;
     }
     if (tid == 0) {
         IterCtrl c;
@@ -1129,8 +1147,9 @@ __device__ __forceinline__ void step_planner(const KgmtDev& d, int t, int expand
 //   epilogue   one barrier: wave counts -> list positions, the R1 / R2New flushes and
 //              the block's packed count.
 template <int AGENT, int OBS>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) void k_step(KgmtDev d, int t,
-                                                                                        int expand) {
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) void k_step(
+    const KgmtDev* __restrict__ dp, int t, int expand) {
+    const KgmtDev& d = *dp;
     extern __shared__ float4 sDyn[];   // [LDS obstacles][prefix: nBlocks + 1 ints]
     __shared__ int sR1P[kMaxR1];
     __shared__ uint32_t sNew[kMaxR2Words];
@@ -1180,7 +1199,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) voi
     // ---- the child's controls (statePropagator.cu:17-21) depend on the slot's stream
     // alone: drawn while the block counts are in flight (stored only for slots < S)
     Xorwow rs{ra.x, ra.y, ra.z, ra.w, rb.x, rb.y};
-    const ChildCtl ctl = draw_controls<AGENT>(rs, d);
+    ChildCtl ctl = draw_controls<AGENT>(rs, d);
+    asm volatile("" : "+v"(ctl.a), "+v"(ctl.steer), "+v"(ctl.dur), "+v"(ctl.dt), "+v"(ctl.tanS));
     int A, jGoal;
     step_scan(d, pk, sPfx, sRed, &A, &jGoal);
     SBMP_STAMP(1);
@@ -1393,7 +1413,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) voi
         const int v = sR1P[tid];   // nR1 == kBlock
         if (v) atomicAdd(&rep[tid], (unsigned long long)(v & 0xffff) | ((unsigned long long)(v >> 16) << 32));
     }
-    uint32_t* const newCur = d.stepR2New + (size_t)(t % 3) * nW;
+    // replicas: a device atomic on one word serialises (~11 ns each); in the early
+    // iterations most blocks set the same few words, so each replica sees 1/kNewReps
+    uint32_t* const newCur = d.stepR2New + ((size_t)(t % 3) * kNewReps + (size_t)(b % kNewReps)) * nW;
     for (int i = tid; i < nW; i += kBlock) {
         const uint32_t w = sNew[i];
         if (w) atomicOr(&newCur[i], w);
@@ -1597,25 +1619,25 @@ static void launch_step_agent(const KgmtDev& d, int t, int expand, int variant, 
     const size_t shm = sizeof(float4) * (size_t)d.nObs + pfx;   // LDS obstacle forms
     const dim3 grid(1 + d.nBlocks), block(kBlock);   // workgroup 0 plans, 1.. expand
     if (d.gridStart) {
-        launch(k_step<AGENT, kObsGrid>, grid, block, pfx, s, tm, d, t, expand);
+        launch(k_step<AGENT, kObsGrid>, grid, block, pfx, s, tm, d.devSelf, t, expand);
     } else if (d.nObs > kMaxLdsObs) {
-        launch(k_step<AGENT, kObsGlobal>, grid, block, pfx, s, tm, d, t, expand);
+        launch(k_step<AGENT, kObsGlobal>, grid, block, pfx, s, tm, d.devSelf, t, expand);
     } else if (d.nObs <= kMaxRegObs && (variant == 0 || variant == 3)) {
         switch (d.nObs) {
-            case 0: launch(k_step<AGENT, kObsReg + 0>, grid, block, pfx, s, tm, d, t, expand); break;
-            case 1: launch(k_step<AGENT, kObsReg + 1>, grid, block, pfx, s, tm, d, t, expand); break;
-            case 2: launch(k_step<AGENT, kObsReg + 2>, grid, block, pfx, s, tm, d, t, expand); break;
-            case 3: launch(k_step<AGENT, kObsReg + 3>, grid, block, pfx, s, tm, d, t, expand); break;
-            case 4: launch(k_step<AGENT, kObsReg + 4>, grid, block, pfx, s, tm, d, t, expand); break;
-            case 5: launch(k_step<AGENT, kObsReg + 5>, grid, block, pfx, s, tm, d, t, expand); break;
-            case 6: launch(k_step<AGENT, kObsReg + 6>, grid, block, pfx, s, tm, d, t, expand); break;
-            case 7: launch(k_step<AGENT, kObsReg + 7>, grid, block, pfx, s, tm, d, t, expand); break;
-            default: launch(k_step<AGENT, kObsReg + 8>, grid, block, pfx, s, tm, d, t, expand); break;
+            case 0: launch(k_step<AGENT, kObsReg + 0>, grid, block, pfx, s, tm, d.devSelf, t, expand); break;
+            case 1: launch(k_step<AGENT, kObsReg + 1>, grid, block, pfx, s, tm, d.devSelf, t, expand); break;
+            case 2: launch(k_step<AGENT, kObsReg + 2>, grid, block, pfx, s, tm, d.devSelf, t, expand); break;
+            case 3: launch(k_step<AGENT, kObsReg + 3>, grid, block, pfx, s, tm, d.devSelf, t, expand); break;
+            case 4: launch(k_step<AGENT, kObsReg + 4>, grid, block, pfx, s, tm, d.devSelf, t, expand); break;
+            case 5: launch(k_step<AGENT, kObsReg + 5>, grid, block, pfx, s, tm, d.devSelf, t, expand); break;
+            case 6: launch(k_step<AGENT, kObsReg + 6>, grid, block, pfx, s, tm, d.devSelf, t, expand); break;
+            case 7: launch(k_step<AGENT, kObsReg + 7>, grid, block, pfx, s, tm, d.devSelf, t, expand); break;
+            default: launch(k_step<AGENT, kObsReg + 8>, grid, block, pfx, s, tm, d.devSelf, t, expand); break;
         }
     } else if (variant == 2) {
-        launch(k_step<AGENT, kObsLds4>, grid, block, shm, s, tm, d, t, expand);
+        launch(k_step<AGENT, kObsLds4>, grid, block, shm, s, tm, d.devSelf, t, expand);
     } else {
-        launch(k_step<AGENT, kObsLds>, grid, block, shm, s, tm, d, t, expand);
+        launch(k_step<AGENT, kObsLds>, grid, block, shm, s, tm, d.devSelf, t, expand);
     }
 }
 

@@ -245,8 +245,11 @@ KgmtPlanner::KgmtPlanner(const sbmp_kgmt_params& p, int nranks, int rank, Exchan
         d.stepPub = alloc<unsigned long long>((size_t)2 * (d.nR1 + d.nR2 / 32));
         d.stepList = alloc<float4>((size_t)2 * d.nBlocks * kBlock * kStepEntry);
         d.stepDelta = alloc<unsigned long long>((size_t)3 * kDeltaReps * d.nR1);
-        d.stepR2New = alloc<uint32_t>((size_t)3 * (d.nR2 / 32));
+        d.stepR2New = alloc<uint32_t>((size_t)3 * kNewReps * (d.nR2 / 32));
+        dDev_ = alloc<KgmtDev>(1);
+        SBMP_HIP(hipHostMalloc(reinterpret_cast<void**>(&dStage_), sizeof(KgmtDev), hipHostMallocDefault));
     }
+    d.devSelf = dDev_;
     d.recCap = expandBlocks_ * kBlock;   // a rank never holds more flagged slots than it owns
     d.recOut = d.sharded ? alloc<float4>((size_t)2 * kRecordF4 * d.recCap) : nullptr;
     for (int q = 0; q < kMaxRanks; ++q) d.recPeer[q] = nullptr;
@@ -310,6 +313,7 @@ KgmtPlanner::~KgmtPlanner() {
     for (void* ptr : allocs_) (void)hipFree(ptr);
     if (poll_) (void)hipHostFree(poll_);
     if (obs_) (void)hipFree(obs_);
+    if (dStage_) (void)hipHostFree(dStage_);
     if (gridStart_) (void)hipFree(gridStart_);
     if (gridBoxes_) (void)hipFree(gridBoxes_);
     if (stream_ && ownStream_) (void)hipStreamDestroy(stream_);
@@ -339,7 +343,7 @@ void KgmtPlanner::begin(const float* initial, const float* goal, const float* d_
         SBMP_HIP(hipMemsetAsync(d.stepCnt, 0, sizeof(int) * 2 * kMaxStepBlocks, s));
         SBMP_HIP(hipMemsetAsync(d.stepPub, 0, sizeof(unsigned long long) * 2 * (d.nR1 + d.nR2 / 32), s));
         SBMP_HIP(hipMemsetAsync(d.stepDelta, 0, sizeof(unsigned long long) * 3 * kDeltaReps * d.nR1, s));
-        SBMP_HIP(hipMemsetAsync(d.stepR2New, 0, sizeof(uint32_t) * 3 * (d.nR2 / 32), s));
+        SBMP_HIP(hipMemsetAsync(d.stepR2New, 0, sizeof(uint32_t) * 3 * kNewReps * (d.nR2 / 32), s));
     }
     SBMP_HIP(hipMemsetAsync(d.R2Snap, 0, sizeof(uint32_t) * (d.nR2 / 32), s));
     SBMP_HIP(hipMemsetAsync(d.R2Valid, 0, sizeof(int) * d.nR2, s));
@@ -431,6 +435,7 @@ void KgmtPlanner::enqueue(int iterations) {
         const int t = take_iteration();
         if (t == 0) break;
         if (d_.stepMode) {
+            upload_dev();
             launch_step(d_, t, 1, p_.agent, expandVariant_, stream_, timing(K_STEP));
             flushed_ = false;
             stage_fold(t);
@@ -488,8 +493,20 @@ void KgmtPlanner::fold_to(int tLast) {
     lastFolded_ = tLast;
 }
 
+// k_step reads the plan struct at d_.devSelf: refresh that copy when d_ changed (at
+// begin(), or a diagnostics switch), from pinned memory not touched while a copy is queued.
+void KgmtPlanner::upload_dev() {
+    if (!dDev_) throw Error(SBMP_ERR_STATE, "k_step: the plan struct has no device copy");
+    if (uploaded_ && std::memcmp(&d_, dStage_, sizeof(KgmtDev)) == 0) return;
+    if (uploaded_) SBMP_HIP(hipStreamSynchronize(stream_));   // the previous copy has been read
+    std::memcpy(dStage_, &d_, sizeof(KgmtDev));
+    SBMP_HIP(hipMemcpyAsync(dDev_, dStage_, sizeof(KgmtDev), hipMemcpyHostToDevice, stream_));
+    uploaded_ = true;
+}
+
 void KgmtPlanner::sync() {
     if (d_.stepMode && begun_ && !flushed_) {   // complete the last iteration (insert, plan t_next)
+        upload_dev();
         launch_step(d_, t_next_, 0, p_.agent, expandVariant_, stream_, KernelTiming());
         flushed_ = true;
     }
@@ -532,6 +549,7 @@ int KgmtPlanner::last_executed(const std::vector<IterCtrl>& c) const {
 bool KgmtPlanner::active() {
     if (!begun_) return false;
     if (d_.stepMode && !flushed_) {   // the flush pass writes ctrl[t_next] and the goal of t_next - 1
+        upload_dev();
         launch_step(d_, t_next_, 0, p_.agent, expandVariant_, stream_, KernelTiming());
         flushed_ = true;
     }

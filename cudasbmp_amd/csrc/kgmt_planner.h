@@ -162,6 +162,10 @@ private:
 
     sbmp_kgmt_params p_;
     KgmtDev d_{};
+    KgmtDev* dDev_ = nullptr;      // the copy k_step reads (d_.devSelf)
+    KgmtDev* dStage_ = nullptr;    // pinned: what was last copied there
+    bool uploaded_ = false;
+    void upload_dev();
     hipStream_t stream_ = nullptr;
     bool ownStream_ = true;
     Exchange* ex_ = nullptr;
