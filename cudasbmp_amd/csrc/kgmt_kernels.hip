@@ -1148,7 +1148,7 @@ __device__ __forceinline__ void step_planner(const KgmtDev& d, int t, int expand
 //              the block's packed count.
 template <int AGENT, int OBS>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) void k_step(
-    const KgmtDev* __restrict__ dp, int t, int expand) {
+    const KgmtDev* __restrict__ dp, int t, int expand, long long* tlBase) {
     const KgmtDev& d = *dp;
     extern __shared__ float4 sDyn[];   // [LDS obstacles][prefix: nBlocks + 1 ints]
     __shared__ int sR1P[kMaxR1];
@@ -1175,24 +1175,37 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) voi
     const int nW = d.nR2 >> 5;
     const int pp = (t - 1) & 1, cp = t & 1;
     const unsigned long long* const pubCur = d.stepPub + (size_t)cp * (d.nR1 + nW);
-    long long* const tl = (d.timeline && t == d.timelineIter && expand)
-                              ? d.timeline + ((size_t)b * (kBlock / kWave) + wave) * kTimelineStamps
-                              : nullptr;
+    // d.timeline if this launch is the traced one (decided on the host: no dependent
+    // loads of the plan struct before the prologue's own)
+    long long* const tl = tlBase ? tlBase + ((size_t)b * (kBlock / kWave) + wave) * kTimelineStamps : nullptr;
     long long stamp[kTimelineStamps] = {0, 0, 0, 0, 0, 0, 0, 0};
 #define SBMP_STAMP(i)                                                                  \
     do {                                                                               \
         if (tl) stamp[i] = (long long)__builtin_amdgcn_s_memrealtime();                \
     } while (0)
+    // The prologue's pointers in one batch of scalar loads (one round trip; loaded
+    // where first used they were five dependent ones)
+    const int* const cntP = d.stepCnt;
+    const IterCtrl* const ctrlP = d.ctrl;
+    const PlannerStatus* const statusP = d.status;
+    const uint4* const rngAP = d.rngA;
+    const uint2* const rngBP = d.rngB;
+    const unsigned long long* const gnewP = d.gnewOut;
+    // (with the plan's scalars from the first 64 B of the struct)
+    asm volatile("" ::"s"(cntP), "s"(ctrlP), "s"(statusP), "s"(rngAP), "s"(rngBP), "s"(gnewP), "s"(d.M),
+                 "s"(d.nBlocks), "s"(d.numIterations), "s"(d.numDisc), "s"(d.nR1), "s"(d.nR2), "s"(d.cap),
+                 "s"(d.fixGNewClear), "s"(d.batchRule), "s"(d.rcpNumDisc), "s"(d.treeState), "s"(d.treeCtrl),
+                 "s"(d.stepList));
     SBMP_STAMP(0);
 
     // ---- loads that depend on nothing else (the control block as a plain load: a
     // waiting scalar load would serialise behind the scan)
-    const int4 pk = *reinterpret_cast<const int4*>(d.stepCnt + (size_t)pp * kMaxStepBlocks + tid * 4);
-    const IterCtrl pc = d.ctrl[t - 1];
-    const int goalIdx = d.status->goalIdx;
-    const uint4 ra = d.rngA[slot];
-    const uint2 rb = d.rngB[slot];
-    const unsigned long long oldWord = (lane == 0) ? d.gnewOut[slot >> 6] : 0ull;
+    const int4 pk = *reinterpret_cast<const int4*>(cntP + (size_t)pp * kMaxStepBlocks + tid * 4);
+    const IterCtrl pc = ctrlP[t - 1];
+    const int goalIdx = statusP->goalIdx;
+    const uint4 ra = rngAP[slot];
+    const uint2 rb = rngBP[slot];
+    const unsigned long long oldWord = (lane == 0) ? gnewP[slot >> 6] : 0ull;
     const float4 obsReg = (kLdsObs && tid < d.nObs) ? d.obstacles[tid] : make_float4(0.f, 0.f, 0.f, 0.f);
     sR1P[tid] = 0;   // nR1 == kBlock
     for (int i = tid; i < nW; i += kBlock) sNew[i] = 0u;
@@ -1618,26 +1631,27 @@ static void launch_step_agent(const KgmtDev& d, int t, int expand, int variant, 
     const size_t pfx = sizeof(int) * ((size_t)d.nBlocks + 1);
     const size_t shm = sizeof(float4) * (size_t)d.nObs + pfx;   // LDS obstacle forms
     const dim3 grid(1 + d.nBlocks), block(kBlock);   // workgroup 0 plans, 1.. expand
+    long long* const tlBase = (d.timeline && t == d.timelineIter && expand) ? d.timeline : nullptr;
     if (d.gridStart) {
-        launch(k_step<AGENT, kObsGrid>, grid, block, pfx, s, tm, d.devSelf, t, expand);
+        launch(k_step<AGENT, kObsGrid>, grid, block, pfx, s, tm, d.devSelf, t, expand, tlBase);
     } else if (d.nObs > kMaxLdsObs) {
-        launch(k_step<AGENT, kObsGlobal>, grid, block, pfx, s, tm, d.devSelf, t, expand);
+        launch(k_step<AGENT, kObsGlobal>, grid, block, pfx, s, tm, d.devSelf, t, expand, tlBase);
     } else if (d.nObs <= kMaxRegObs && (variant == 0 || variant == 3)) {
         switch (d.nObs) {
-            case 0: launch(k_step<AGENT, kObsReg + 0>, grid, block, pfx, s, tm, d.devSelf, t, expand); break;
-            case 1: launch(k_step<AGENT, kObsReg + 1>, grid, block, pfx, s, tm, d.devSelf, t, expand); break;
-            case 2: launch(k_step<AGENT, kObsReg + 2>, grid, block, pfx, s, tm, d.devSelf, t, expand); break;
-            case 3: launch(k_step<AGENT, kObsReg + 3>, grid, block, pfx, s, tm, d.devSelf, t, expand); break;
-            case 4: launch(k_step<AGENT, kObsReg + 4>, grid, block, pfx, s, tm, d.devSelf, t, expand); break;
-            case 5: launch(k_step<AGENT, kObsReg + 5>, grid, block, pfx, s, tm, d.devSelf, t, expand); break;
-            case 6: launch(k_step<AGENT, kObsReg + 6>, grid, block, pfx, s, tm, d.devSelf, t, expand); break;
-            case 7: launch(k_step<AGENT, kObsReg + 7>, grid, block, pfx, s, tm, d.devSelf, t, expand); break;
-            default: launch(k_step<AGENT, kObsReg + 8>, grid, block, pfx, s, tm, d.devSelf, t, expand); break;
+            case 0: launch(k_step<AGENT, kObsReg + 0>, grid, block, pfx, s, tm, d.devSelf, t, expand, tlBase); break;
+            case 1: launch(k_step<AGENT, kObsReg + 1>, grid, block, pfx, s, tm, d.devSelf, t, expand, tlBase); break;
+            case 2: launch(k_step<AGENT, kObsReg + 2>, grid, block, pfx, s, tm, d.devSelf, t, expand, tlBase); break;
+            case 3: launch(k_step<AGENT, kObsReg + 3>, grid, block, pfx, s, tm, d.devSelf, t, expand, tlBase); break;
+            case 4: launch(k_step<AGENT, kObsReg + 4>, grid, block, pfx, s, tm, d.devSelf, t, expand, tlBase); break;
+            case 5: launch(k_step<AGENT, kObsReg + 5>, grid, block, pfx, s, tm, d.devSelf, t, expand, tlBase); break;
+            case 6: launch(k_step<AGENT, kObsReg + 6>, grid, block, pfx, s, tm, d.devSelf, t, expand, tlBase); break;
+            case 7: launch(k_step<AGENT, kObsReg + 7>, grid, block, pfx, s, tm, d.devSelf, t, expand, tlBase); break;
+            default: launch(k_step<AGENT, kObsReg + 8>, grid, block, pfx, s, tm, d.devSelf, t, expand, tlBase); break;
         }
     } else if (variant == 2) {
-        launch(k_step<AGENT, kObsLds4>, grid, block, shm, s, tm, d.devSelf, t, expand);
+        launch(k_step<AGENT, kObsLds4>, grid, block, shm, s, tm, d.devSelf, t, expand, tlBase);
     } else {
-        launch(k_step<AGENT, kObsLds>, grid, block, shm, s, tm, d.devSelf, t, expand);
+        launch(k_step<AGENT, kObsLds>, grid, block, shm, s, tm, d.devSelf, t, expand, tlBase);
     }
 }
 
