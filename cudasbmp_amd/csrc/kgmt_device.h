@@ -191,6 +191,22 @@ struct KgmtDev {
     const KgmtDev* devSelf;
 };
 
+// Global-address-space view of a device pointer.  A pointer loaded from the plan
+// struct in device memory (k_step reads it there) is generic to the compiler: its
+// accesses become flat_* instructions, which take no scalar base, count against
+// lgkmcnt (so every LDS / scalar wait also waits for them) and check the apertures.
+// (The qualifier exists only in the device pass: hipcc also parses kernel bodies for
+// the host, where address-space-qualified vector copies do not compile.)
+#if defined(__HIP_DEVICE_COMPILE__)
+#define SBMP_GAS __attribute__((address_space(1)))
+#else
+#define SBMP_GAS
+#endif
+template <class T>
+__device__ __forceinline__ SBMP_GAS T* G(T* p) {
+    return (SBMP_GAS T*)p;
+}
+
 // 16-B / 8-B stores with sc1: written through to memory during the kernel, so the
 // dependent kernel boundary has fewer dirty L2 lines to write back (MI355X_MICROARCH.md,
 // "boundary": + dirty bytes / 6 TB/s).  Raw buffer stores carry the cache policy as a

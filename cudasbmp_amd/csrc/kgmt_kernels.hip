@@ -853,7 +853,7 @@ size_t oneshot_inbox_words(long long n, int nranks) { return (size_t)2 * nranks 
 // expand == 0 is the flush pass run before a read-back (no expansion; the same
 // values are rewritten by k_step(t) proper, so it is idempotent).
 // OR of word w over the kNewReps R2New replicas ([rep][nW] layout: one line per replica)
-__device__ __forceinline__ uint32_t merge_new(const uint32_t* p, int nW, int w) {
+__device__ __forceinline__ uint32_t merge_new(const SBMP_GAS uint32_t* p, int nW, int w) {
     uint32_t v = 0u;
 #pragma unroll
     for (int r = 0; r < kNewReps; ++r) v |= p[(size_t)r * nW + w];
@@ -889,7 +889,8 @@ __device__ __forceinline__ void step_scan(const KgmtDev& d, int4 pk, int* sPfx, 
     __syncthreads();
     int base = incl - run;
     base += (wave > 0 ? sRed[0][0] : 0) + (wave > 1 ? sRed[0][1] : 0) + (wave > 2 ? sRed[0][2] : 0);
-    *A = sRed[0][0] + sRed[0][1] + sRed[0][2] + sRed[0][3];
+    // uniform by construction; readfirstlane so the plan that follows is scalar code
+    *A = __builtin_amdgcn_readfirstlane(sRed[0][0] + sRed[0][1] + sRed[0][2] + sRed[0][3]);
     // Prefixes grow with g and a goal child's in-block index is below its block's
     // count, so the lowest g holding a goal child has the lowest global index.
     int gmin = kNoGoalIdx;
@@ -904,7 +905,7 @@ __device__ __forceinline__ void step_scan(const KgmtDev& d, int4 pk, int* sPfx, 
     gmin = first_lane_value(gmin != kNoGoalIdx, gmin, kNoGoalIdx);
     if (lane == 0) sRed[1][wave] = gmin;
     __syncthreads();
-    *jGoal = min(min(sRed[1][0], sRed[1][1]), min(sRed[1][2], sRed[1][3]));
+    *jGoal = __builtin_amdgcn_readfirstlane(min(min(sRed[1][0], sRed[1][1]), min(sRed[1][2], sRed[1][3])));
 }
 
 // Plan scalars of iteration t from t-1's control block and the scan (KGMT.cu:118,
@@ -955,20 +956,20 @@ __device__ __forceinline__ void step_planner(const KgmtDev& d, int t, int expand
     const int cell = min(tid, d.nR1 - 1);
     const bool own = tid < d.nR1;
     const bool tl = d.timelineFin && t == d.timelineIter && tid == 0;   // diagnostics: entry, publish
-    if (tl) d.timelineFin[0] = (long long)__builtin_amdgcn_s_memrealtime();
+    if (tl) G(d.timelineFin)[0] = (long long)__builtin_amdgcn_s_memrealtime();
     // every input at entry
-    const int4 pk = *reinterpret_cast<const int4*>(d.stepCnt + (size_t)pp * kMaxStepBlocks + tid * 4);
-    const IterCtrl pc = d.ctrl[t - 1];
-    const int goalIdx = d.status->goalIdx;
-    const int* tabPrev = d.R1 + (size_t)pp * 5 * d.nR1;
+    const int4 pk = *reinterpret_cast<const SBMP_GAS int4*>(G(d.stepCnt) + (size_t)pp * kMaxStepBlocks + tid * 4);
+    const IterCtrl pc = G(d.ctrl)[t - 1];
+    const int goalIdx = G(d.status)->goalIdx;
+    const SBMP_GAS int* tabPrev = G(d.R1) + (size_t)pp * 5 * d.nR1;
     int r1 = tabPrev[cell], r1a = tabPrev[d.nR1 + cell], r1v = tabPrev[2 * d.nR1 + cell],
         r1i = tabPrev[3 * d.nR1 + cell], r1c = tabPrev[4 * d.nR1 + cell];
-    const unsigned long long* deltaPrev = d.stepDelta + (size_t)((t - 1) % 3) * kDeltaReps * d.nR1;
+    const SBMP_GAS unsigned long long* deltaPrev = G(d.stepDelta) + (size_t)((t - 1) % 3) * kDeltaReps * d.nR1;
     unsigned long long dl = 0ull;   // replicas: carry-free sums
 #pragma unroll
     for (int r = 0; r < kDeltaReps; ++r) dl += deltaPrev[(size_t)r * d.nR1 + cell];
-    const uint32_t* availPrev = d.R2Avail + (size_t)pp * nW;
-    const uint32_t* newPrev = d.stepR2New + (size_t)((t - 1) % 3) * kNewReps * nW;
+    const SBMP_GAS uint32_t* availPrev = G(d.R2Avail) + (size_t)pp * nW;
+    const SBMP_GAS uint32_t* newPrev = G(d.stepR2New) + (size_t)((t - 1) % 3) * kNewReps * nW;
     uint32_t availW[kW], newW[kW];
 #pragma unroll
     for (int j = 0; j < kW; ++j) {
@@ -990,15 +991,15 @@ __device__ __forceinline__ void step_planner(const KgmtDev& d, int t, int expand
     int A, jGoal;
     step_scan(d, pk, sPfx, sRed, &A, &jGoal);
     const StepPlan q = step_plan(d, t, expand, pc, goalIdx, A, jGoal);
-    int* tabCur = d.R1 + (size_t)cp * 5 * d.nR1;
+    SBMP_GAS int* tabCur = G(d.R1) + (size_t)cp * 5 * d.nR1;
     if (!q.ranPrev) {   // t-1 did not run: the loop has ended; carry the tables forward
         for (int i = tid; i < 5 * d.nR1; i += kBlock) tabCur[i] = tabPrev[i];
-        for (int i = tid; i < nW; i += kBlock) d.R2Avail[(size_t)cp * nW + i] = availPrev[i];
+        for (int i = tid; i < nW; i += kBlock) G(d.R2Avail)[(size_t)cp * nW + i] = availPrev[i];
         if (tid == 0) {
             IterCtrl c{};
             c.run = 0;
             c.H = pc.H;
-            d.ctrl[t] = c;
+            G(d.ctrl)[t] = c;
         }
         return;
     }
@@ -1055,7 +1056,7 @@ __device__ __forceinline__ void step_planner(const KgmtDev& d, int t, int expand
         scv = (r1a == 0) ? 1.0f : sc / total;
     }
     // publish first (tagged 8-B words, written through)
-    unsigned long long* const pub = d.stepPub + (size_t)cp * (d.nR1 + nW);
+    SBMP_GAS unsigned long long* const pub = G(d.stepPub) + (size_t)cp * (d.nR1 + nW);
     const unsigned long long tag = (unsigned long long)(unsigned)t << 32;
     if (q.executes) {
         if (own) __hip_atomic_store(pub + cell, tag | __float_as_uint(scv), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1066,24 +1067,24 @@ __device__ __forceinline__ void step_planner(const KgmtDev& d, int t, int expand
                 __hip_atomic_store(pub + d.nR1 + w, tag | snapW[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
-    if (tl) d.timelineFin[1] = (long long)__builtin_amdgcn_s_memrealtime();
+    if (tl) G(d.timelineFin)[1] = (long long)__builtin_amdgcn_s_memrealtime();
     if (own) {
         tabCur[cell] = r1;
         tabCur[d.nR1 + cell] = r1a;
         tabCur[2 * d.nR1 + cell] = r1v;
         tabCur[3 * d.nR1 + cell] = r1i;
         tabCur[4 * d.nR1 + cell] = r1c;
-        if (q.runT) d.R1Score[cp * d.nR1 + cell] = scv;
+        if (q.runT) G(d.R1Score)[cp * d.nR1 + cell] = scv;
     }
 #pragma unroll
     for (int j = 0; j < kW; ++j) {
         const int w = tid + j * kBlock;
-        if (j * kBlock < nW && w < nW) d.R2Avail[(size_t)cp * nW + w] = snapW[j];
+        if (j * kBlock < nW && w < nW) G(d.R2Avail)[(size_t)cp * nW + w] = snapW[j];
     }
     {   // ring (t+1) % 3, last read by k_step(t-1): zero for k_step(t+1)
-        unsigned long long* zd = d.stepDelta + (size_t)((t + 1) % 3) * kDeltaReps * d.nR1;
+        SBMP_GAS unsigned long long* zd = G(d.stepDelta) + (size_t)((t + 1) % 3) * kDeltaReps * d.nR1;
         for (int i = tid; i < kDeltaReps * d.nR1; i += kBlock) zd[i] = 0ull;
-        uint32_t* zn = d.stepR2New + (size_t)((t + 1) % 3) * kNewReps * nW;
+        SBMP_GAS uint32_t* zn = G(d.stepR2New) + (size_t)((t + 1) % 3) * kNewReps * nW;
         for (int i = tid; i < kNewReps * nW; i += kBlock) zn[i] = 0u;
     }
     if (tid == 0) {
@@ -1100,16 +1101,16 @@ __device__ __forceinline__ void step_planner(const KgmtDev& d, int t, int expand
         c.A = 0;
         c.scoreBuf = cp;
         for (int i = 0; i < 5; ++i) c.pad[i] = 0;
-        d.ctrl[t] = c;
-        if (t > 1) d.ctrl[t - 1].A = A;
-        if (q.newGoal != goalIdx) d.status->goalIdx = q.newGoal;
+        G(d.ctrl)[t] = c;
+        if (t > 1) G(d.ctrl)[t - 1].A = A;
+        if (q.newGoal != goalIdx) G(d.status)->goalIdx = q.newGoal;
     }
     // Insert t-1's flagged children (rows tsPrev + j, KGMT.cu:540-593) when they are
     // few: everything above is what the expanders wait for, and from here on this
     // workgroup is idle.
     if (t > 1 && A <= kPlannerInsertMax) {
         const int n = min(q.nIns, d.M - q.tsPrev);   // D13: the reference writes past M
-        const float4* listPrev = d.stepList + (size_t)pp * d.nBlocks * kBlock * kStepEntry;
+        const SBMP_GAS float4* listPrev = G(d.stepList) + (size_t)pp * d.nBlocks * kBlock * kStepEntry;
         // list entry of row j: block lo with sPfx[lo] <= j < sPfx[lo + 1]
         auto entry = [&](int j) {
             int lo = 0;
@@ -1119,14 +1120,14 @@ __device__ __forceinline__ void step_planner(const KgmtDev& d, int t, int expand
         };
         auto put = [&](int j, float4 s4, float4 u4, float c) {
             const int dst = q.tsPrev + j;
-            d.treeState[dst] = s4;
-            d.treeCtrl[dst] = make_float4(u4.x, u4.y, u4.z, c);   // cost = parent's + duration (KGMT.cu:631-633)
-            d.treeParent[dst] = __float_as_int(u4.w);
+            G(d.treeState)[dst] = s4;
+            G(d.treeCtrl)[dst] = make_float4(u4.x, u4.y, u4.z, c);   // cost = parent's + duration (KGMT.cu:631-633)
+            G(d.treeParent)[dst] = __float_as_int(u4.w);
         };
         for (int j0 = tid; j0 < n; j0 += 2 * kBlock) {   // two rows per thread per round, loads first
             const int j1 = j0 + kBlock;
-            const float4* e0 = entry(j0);
-            const float4* e1 = entry(min(j1, n - 1));
+            const SBMP_GAS float4* e0 = entry(j0);
+            const SBMP_GAS float4* e1 = entry(min(j1, n - 1));
             const float4 s0 = e0[0], u0 = e0[1], s1 = e1[0], u1 = e1[1];
             const float c0 = e0[2].x, c1 = e1[2].x;
             put(j0, s0, u0, c0);
@@ -1174,7 +1175,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) voi
     const int slot = b * kBlock + tid;
     const int nW = d.nR2 >> 5;
     const int pp = (t - 1) & 1, cp = t & 1;
-    const unsigned long long* const pubCur = d.stepPub + (size_t)cp * (d.nR1 + nW);
+    const SBMP_GAS unsigned long long* const pubCur = G(d.stepPub) + (size_t)cp * (d.nR1 + nW);
     // d.timeline if this launch is the traced one (decided on the host: no dependent
     // loads of the plan struct before the prologue's own)
     long long* const tl = tlBase ? tlBase + ((size_t)b * (kBlock / kWave) + wave) * kTimelineStamps : nullptr;
@@ -1185,12 +1186,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) voi
     } while (0)
     // The prologue's pointers in one batch of scalar loads (one round trip; loaded
     // where first used they were five dependent ones)
-    const int* const cntP = d.stepCnt;
-    const IterCtrl* const ctrlP = d.ctrl;
-    const PlannerStatus* const statusP = d.status;
-    const uint4* const rngAP = d.rngA;
-    const uint2* const rngBP = d.rngB;
-    const unsigned long long* const gnewP = d.gnewOut;
+    const SBMP_GAS int* const cntP = G(d.stepCnt);
+    const SBMP_GAS IterCtrl* const ctrlP = G(d.ctrl);
+    const SBMP_GAS PlannerStatus* const statusP = G(d.status);
+    const SBMP_GAS uint4* const rngAP = G(d.rngA);
+    const SBMP_GAS uint2* const rngBP = G(d.rngB);
+    const SBMP_GAS unsigned long long* const gnewP = G(d.gnewOut);
     // (with the plan's scalars from the first 64 B of the struct)
     asm volatile("" ::"s"(cntP), "s"(ctrlP), "s"(statusP), "s"(rngAP), "s"(rngBP), "s"(gnewP), "s"(d.M),
                  "s"(d.nBlocks), "s"(d.numIterations), "s"(d.numDisc), "s"(d.nR1), "s"(d.nR2), "s"(d.cap),
@@ -1200,13 +1201,14 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) voi
 
     // ---- loads that depend on nothing else (the control block as a plain load: a
     // waiting scalar load would serialise behind the scan)
-    const int4 pk = *reinterpret_cast<const int4*>(cntP + (size_t)pp * kMaxStepBlocks + tid * 4);
+    const int4 pk = *reinterpret_cast<const SBMP_GAS int4*>(cntP + (size_t)pp * kMaxStepBlocks + tid * 4);
     const IterCtrl pc = ctrlP[t - 1];
     const int goalIdx = statusP->goalIdx;
     const uint4 ra = rngAP[slot];
     const uint2 rb = rngBP[slot];
     const unsigned long long oldWord = (lane == 0) ? gnewP[slot >> 6] : 0ull;
-    const float4 obsReg = (kLdsObs && tid < d.nObs) ? d.obstacles[tid] : make_float4(0.f, 0.f, 0.f, 0.f);
+    float4 obsReg = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (kLdsObs && tid < d.nObs) obsReg = G(d.obstacles)[tid];
     sR1P[tid] = 0;   // nR1 == kBlock
     for (int i = tid; i < nW; i += kBlock) sNew[i] = 0u;
     // ---- the child's controls (statePropagator.cu:17-21) depend on the slot's stream
@@ -1217,7 +1219,15 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) voi
     int A, jGoal;
     step_scan(d, pk, sPfx, sRed, &A, &jGoal);
     SBMP_STAMP(1);
-    const StepPlan q = step_plan(d, t, expand, pc, goalIdx, A, jGoal);
+    // the control block and the goal index were loaded per lane (vector loads do not
+    // wait behind the scan's scalar work); the plan is wave-uniform, so scalar code
+    IterCtrl pcu = pc;
+    pcu.executed = __builtin_amdgcn_readfirstlane(pc.executed);
+    pcu.treeSize = __builtin_amdgcn_readfirstlane(pc.treeSize);
+    pcu.gLo = __builtin_amdgcn_readfirstlane(pc.gLo);
+    pcu.nExp = __builtin_amdgcn_readfirstlane(pc.nExp);
+    pcu.H = __builtin_amdgcn_readfirstlane(pc.H);
+    const StepPlan q = step_plan(d, t, expand, pcu, __builtin_amdgcn_readfirstlane(goalIdx), A, jGoal);
     if (!q.ranPrev) return;
 
     // ---- D6 clear of this block's words of t-1 (KGMT.cu:231,556)
@@ -1239,20 +1249,20 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) voi
             const int j = sPfx[b] + tid;
             const int dst = q.tsPrev + j;
             if (j < q.nIns && dst < d.M) {   // D13: the reference writes past M here
-                const float4* e =
-                    d.stepList + ((size_t)pp * d.nBlocks * kBlock + (size_t)b * kBlock + tid) * kStepEntry;
+                const SBMP_GAS float4* e =
+                    G(d.stepList) + ((size_t)pp * d.nBlocks * kBlock + (size_t)b * kBlock + tid) * kStepEntry;
                 const float4 s4 = e[0];
                 const float4 u4 = e[1];
                 const float4 m4 = e[2];
-                d.treeState[dst] = s4;
-                d.treeCtrl[dst] = make_float4(u4.x, u4.y, u4.z, m4.x);   // cost = parent's + duration (KGMT.cu:631-633)
-                d.treeParent[dst] = __float_as_int(u4.w);
+                G(d.treeState)[dst] = s4;
+                G(d.treeCtrl)[dst] = make_float4(u4.x, u4.y, u4.z, m4.x);   // cost = parent's + duration (KGMT.cu:631-633)
+                G(d.treeParent)[dst] = __float_as_int(u4.w);
             }
         }
     };
     if (!doExpand) {
         insert_prev();
-        if (lane == 0 && word != oldWord) d.gnewOut[slot >> 6] = word;
+        if (lane == 0 && word != oldWord) G(d.gnewOut)[slot >> 6] = word;
         return;
     }
 
@@ -1260,8 +1270,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) voi
     const bool act = slot < q.S;
     const int g = !act ? 0 : slot_div(d, slot, q.k);   // slot = g*k + i
     const int parent = act ? q.gLo + g : 0;
-    const float4* src = d.treeState + parent;   // the parent's state, and its cost
-    const float* srcCost = &d.treeCtrl[parent].w;
+    const SBMP_GAS float4* src = G(d.treeState) + parent;   // the parent's state, and its cost
+    const SBMP_GAS float* srcCost = &G(d.treeCtrl)[parent].w;
     // A parent inserted by t-1 is read from its block's compacted list: block lo with
     // sPfx[lo] <= j < sPfx[lo + 1].  j grows with the lane; when a wave's parents are
     // at most two consecutive list positions jA, jB (k >= 32 children per parent) both
@@ -1292,8 +1302,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) voi
             }
         }
         if (fromList) {
-            src = d.stepList + ((size_t)pp * d.nBlocks * kBlock + (size_t)lo * kBlock + (j - sPfx[lo])) * kStepEntry;
-            srcCost = reinterpret_cast<const float*>(src + 2);
+            src = G(d.stepList) + ((size_t)pp * d.nBlocks * kBlock + (size_t)lo * kBlock + (j - sPfx[lo])) * kStepEntry;
+            srcCost = reinterpret_cast<const SBMP_GAS float*>(src + 2);
         }
     }
     // Parent and obstacles are issued back to back and waited for together.
@@ -1301,11 +1311,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) voi
     const float parentCost = *srcCost;
     float4 ro[kRegObs > 0 ? kRegObs : 1];
 #pragma unroll
-    for (int i = 0; i < kRegObs; ++i) ro[i] = d.obstacles[i];
+    for (int i = 0; i < kRegObs; ++i) ro[i] = G(d.obstacles)[i];
     insert_prev();
     if (kLdsObs) {
         if (tid < d.nObs) sObs[tid] = obsReg;
-        for (int i = tid + kBlock; i < d.nObs; i += kBlock) sObs[i] = d.obstacles[i];
+        for (int i = tid + kBlock; i < d.nObs; i += kBlock) sObs[i] = G(d.obstacles)[i];
         __syncthreads();
     }
     SBMP_STAMP(2);
@@ -1350,10 +1360,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) voi
         store_wt(d.rngB, slot, make_uint2(rs.v4, rs.d));
         if (q1 >= 0) atomicAdd(&sR1P[q1], valid ? 1 : 0x10000);
         if (d.r2log) {
-            d.r2log[(size_t)(t % kFoldEvery) * d.logSlots + b * kBlock + tid] =
+            G(d.r2log)[(size_t)(t % kFoldEvery) * d.logSlots + b * kBlock + tid] =
                 (q2 >= 0) ? (uint16_t)(q2 | (valid ? 0x8000 : 0)) : kNoKey;
         } else if (q2 >= 0) {
-            atomicAdd(valid ? &d.R2Valid[q2] : &d.R2Invalid[q2], 1);
+            __hip_atomic_fetch_add(G(valid ? d.R2Valid : d.R2Invalid) + q2, 1, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
         }
     }
     {   // tags must read t; a word read before the planner published it is re-read (bounded)
@@ -1370,7 +1381,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) voi
                 }
                 if (__ballot(stale) == 0ull) break;
                 if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > kStepWaitTicks) {   // give up, report
-                    if (stale) atomicExch(&d.status->error, kErrStepHandoff);
+                    if (stale)
+                        __hip_atomic_exchange(&G(d.status)->error, kErrStepHandoff, __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_AGENT);
                     break;
                 }
             }
@@ -1392,9 +1405,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) voi
     const bool flagged = (wordAll >> lane) & 1ull;
     if (__ballot(flagged && !act) != 0ull) {   // rare; keeps the wait below off the common path
         if (flagged && !act) {   // a stale flag on a slot past S: the child last written there
-            cs = d.uState[slot];
-            cc = d.uCtrl[slot];
-            cost = d.treeCtrl[__float_as_int(cc.w)].w + cc.z;
+            cs = G(d.uState)[slot];
+            cc = G(d.uCtrl)[slot];
+            cost = G(d.treeCtrl)[__float_as_int(cc.w)].w + cc.z;
         }
     }
     bool inGoal = false;
@@ -1406,7 +1419,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) voi
     const int idxW = __popcll(wordAll & ((1ull << lane) - 1ull));
     const int glW = first_lane_value(flagged && inGoal, idxW, kNoGoalIdx);
     if (lane == 0) {
-        d.gnewOut[slot >> 6] = wordAll;
+        G(d.gnewOut)[slot >> 6] = wordAll;
         sWaveCnt[wave] = __popcll(wordAll);
         sWaveGoal[wave] = glW;
     }
@@ -1415,23 +1428,25 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) voi
     const int c0 = sWaveCnt[0], c1 = sWaveCnt[1], c2 = sWaveCnt[2], c3 = sWaveCnt[3];
     const int waveOff = (wave > 0 ? c0 : 0) + (wave > 1 ? c1 : 0) + (wave > 2 ? c2 : 0);
     if (flagged) {
-        float4* e = d.stepList + ((size_t)cp * d.nBlocks * kBlock + (size_t)b * kBlock + waveOff + idxW) * kStepEntry;
+        SBMP_GAS float4* e = G(d.stepList) + ((size_t)cp * d.nBlocks * kBlock + (size_t)b * kBlock + waveOff + idxW) * kStepEntry;
         e[0] = cs;
         e[1] = cc;
         e[2] = make_float4(cost, 0.0f, 0.0f, 0.0f);
     }
     {   // one 64-bit atomic per touched cell, into this workgroup's replica
-        unsigned long long* const rep =
-            d.stepDelta + (size_t)(t % 3) * kDeltaReps * d.nR1 + (size_t)(b % kDeltaReps) * d.nR1;
+        SBMP_GAS unsigned long long* const rep =
+            G(d.stepDelta) + (size_t)(t % 3) * kDeltaReps * d.nR1 + (size_t)(b % kDeltaReps) * d.nR1;
         const int v = sR1P[tid];   // nR1 == kBlock
-        if (v) atomicAdd(&rep[tid], (unsigned long long)(v & 0xffff) | ((unsigned long long)(v >> 16) << 32));
+        if (v)
+            __hip_atomic_fetch_add(rep + tid, (unsigned long long)(v & 0xffff) | ((unsigned long long)(v >> 16) << 32),
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     // replicas: a device atomic on one word serialises (~11 ns each); in the early
     // iterations most blocks set the same few words, so each replica sees 1/kNewReps
-    uint32_t* const newCur = d.stepR2New + ((size_t)(t % 3) * kNewReps + (size_t)(b % kNewReps)) * nW;
+    SBMP_GAS uint32_t* const newCur = G(d.stepR2New) + ((size_t)(t % 3) * kNewReps + (size_t)(b % kNewReps)) * nW;
     for (int i = tid; i < nW; i += kBlock) {
         const uint32_t w = sNew[i];
-        if (w) atomicOr(&newCur[i], w);
+        if (w) __hip_atomic_fetch_or(newCur + i, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     if (tid == 0) {   // the block's flagged count and its lowest goal child (in-block index)
         const int g0 = sWaveGoal[0], g1 = sWaveGoal[1], g2 = sWaveGoal[2], g3 = sWaveGoal[3];
@@ -1440,7 +1455,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) voi
         if (g2 != kNoGoalIdx) gmin = c0 + c1 + g2;
         if (g1 != kNoGoalIdx) gmin = c0 + g1;
         if (g0 != kNoGoalIdx) gmin = g0;
-        d.stepCnt[(size_t)cp * kMaxStepBlocks + b] = (c0 + c1 + c2 + c3) | ((gmin == kNoGoalIdx ? 0 : gmin + 1) << 16);
+        G(d.stepCnt)[(size_t)cp * kMaxStepBlocks + b] = (c0 + c1 + c2 + c3) | ((gmin == kNoGoalIdx ? 0 : gmin + 1) << 16);
     }
     SBMP_STAMP(6);
     if (tl) {
@@ -1450,7 +1465,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) voi
         stamp[7] = ((long long)xcc << 32) | hw;
     }
     if (tl && lane == 0)
-        for (int i = 0; i < kTimelineStamps; ++i) tl[i] = stamp[i];
+        for (int i = 0; i < kTimelineStamps; ++i) G(tl)[i] = stamp[i];
 #undef SBMP_STAMP
 }
 
