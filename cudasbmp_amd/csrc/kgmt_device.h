@@ -703,8 +703,9 @@ __device__ __forceinline__ bool point_euler(float4 p, const ChildCtl& ctl, const
 //   - isBroadPhaseValid (collisionCheck.cu:6-14) as the separation metric of wave_cull
 //     (exact for finite operands; a NaN box list never takes this loop), one uniform
 //     branch per box the wave's cull kept, the metric a float (no lane-mask merge);
-//   - sincos_pred: Cody-Waite on every lane, Payne-Hanek only for a lane past 105615
-//     (a steering angle near +-pi/2 makes theta grow that far within a child).
+//   - sincos: Cody-Waite alone when car_theta_bounded holds on every lane (nearly
+//     every wave), else sincos_pred: Cody-Waite on every lane and Payne-Hanek only for
+//     a lane past 105615 (a steering angle near +-pi/2 makes theta grow that far).
 // The results are those of car_euler bit for bit (the same operations on the same
 // values; the tests only replace comparisons by exact equivalents).
 
@@ -727,7 +728,20 @@ __device__ __forceinline__ float box_sep(sbmp_f32x2 mn, sbmp_f32x2 mx, float4 o)
 // and no NaN box (the separation metric ignores NaN).  Per plan, so wave-uniform.
 __device__ __forceinline__ bool car_fast_ok(const KgmtDev& d) { return d.invAgentLength != 0.0f && !d.obsNaN; }
 
-template <int OBS>
+// true if no Euler step of this child can take theta past 100000 (so Cody-Waite
+// alone reduces it): |theta_k| <= |theta_0| + T / L |tan steer| (|v_0| + |a| T), with
+// a 5% margin below 105615 for the float rounding of the steps and of this bound.
+// NaN / inf inputs fail it.
+__device__ __forceinline__ bool car_theta_bounded(float4 p, const ChildCtl& ctl, const KgmtDev& d) {
+    const float T = ctl.dur;
+    const float B = __builtin_fabsf(p.z) +
+                    T * d.invAgentLength * __builtin_fabsf(ctl.tanS) * (__builtin_fabsf(p.w) + __builtin_fabsf(ctl.a) * T);
+    return B < 100000.0f;
+}
+
+// PH: some lane of the wave may pass 105615 (car_theta_bounded failed): sincos_pred's
+// per-step check and Payne-Hanek branch; otherwise Cody-Waite alone.
+template <int OBS, bool PH>
 __device__ __forceinline__ bool car_euler_fast(float4 p, const ChildCtl& ctl, const KgmtDev& d, const float4* obs,
                                                ChildOut& out) {
     constexpr int NOBS = obs_in_registers(OBS);
@@ -745,7 +759,8 @@ __device__ __forceinline__ bool car_euler_fast(float4 p, const ChildCtl& ctl, co
         // a 64-bit lane mask in scalar registers for the whole loop
         if (NOBS > 1) asm volatile("" : "+s"(kept));   // (one box: a single flag either way)
         float st, ct;
-        sincos_pred(vt.y, &st, &ct);   // Payne-Hanek for the rare lane past 105615 (a huge steering tan)
+        if constexpr (PH) sincos_pred(vt.y, &st, &ct);   // Payne-Hanek for the rare lane past 105615
+        else sincos_cw(vt.y, &st, &ct);
         const sbmp_f32x2 nxy = __builtin_elementwise_fma(sbmp_f32x2{vt.x, vt.x} * sbmp_f32x2{ct, st}, dt2, xy);
         const sbmp_f32x2 far = wh - nxy;   // W - x, H - y
         const float vl = vt.x * invL;     // v / L, exact for a power-of-two L
@@ -765,7 +780,9 @@ __device__ __forceinline__ bool car_euler_fast(float4 p, const ChildCtl& ctl, co
         const bool upd = in4 > 0.0f;   // alive & inside
         xy = live ? nxy : xy;
         vt = upd ? nvt : vt;
-        aliveF = (upd & (sep >= 0.0f)) ? 1.0f : 0.0f;
+        // > 0 iff upd and sep >= 0: sep + 2^-149 > 0 iff sep >= 0 (f32 denormals on;
+        // sep is never NaN, a min from 1), and no lane mask is combined on the SALU
+        aliveF = seg_min(in4, sep + 0x1p-149f);
     }
     asm volatile("" : "+v"(aliveF));   // keep the last step's masks from living across the loop
     out.state = make_float4(xy.x, xy.y, vt.y, vt.x);

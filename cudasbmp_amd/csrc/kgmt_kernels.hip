@@ -1328,7 +1328,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) voi
     bool fast = false;
     if constexpr (AGENT == 0 && kRegObs > 0) {
         fast = car_fast_ok(d);   // per plan (uniform)
-        if (fast) valid = car_euler_fast<OBS>(p, ctl, d, obs, out) && act;
+        if (fast) {
+            // a huge steering tan can drive theta past Cody-Waite's range within a child
+            if (__ballot(!car_theta_bounded(p, ctl, d)) == 0ull) valid = car_euler_fast<OBS, false>(p, ctl, d, obs, out) && act;
+            else valid = car_euler_fast<OBS, true>(p, ctl, d, obs, out) && act;
+        }
     }
     if (!fast && act)
         valid = (AGENT == 0) ? car_euler<OBS>(p, ctl, d, obs, out) : point_euler<OBS>(p, ctl, d, obs, out);
