@@ -96,6 +96,22 @@ __device__ __forceinline__ float4 load_record(const float4* p) {
                        __uint_as_float((uint32_t)b), __uint_as_float((uint32_t)(b >> 32)));
 }
 
+// The same two forms for a global-address-space pointer (sharded k_step lists).
+__device__ __forceinline__ float4 load_record_g(const SBMP_GAS float4* p) {
+    const SBMP_GAS unsigned long long* q = reinterpret_cast<const SBMP_GAS unsigned long long*>(p);
+    const unsigned long long a = __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    const unsigned long long b = __hip_atomic_load(q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    return make_float4(__uint_as_float((uint32_t)a), __uint_as_float((uint32_t)(a >> 32)),
+                       __uint_as_float((uint32_t)b), __uint_as_float((uint32_t)(b >> 32)));
+}
+__device__ __forceinline__ void store_record_g(SBMP_GAS float4* p, float4 v) {
+    SBMP_GAS unsigned long long* q = reinterpret_cast<SBMP_GAS unsigned long long*>(p);
+    __hip_atomic_store(q, ((unsigned long long)__float_as_uint(v.y) << 32) | __float_as_uint(v.x), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(q + 1, ((unsigned long long)__float_as_uint(v.w) << 32) | __float_as_uint(v.z),
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 // ------------------------------------------------------------------ expand
 // A sharded record word pair, stored through to memory (peers read it over xGMI).
 __device__ __forceinline__ void store_record(float4* p, float4 v) {
@@ -908,6 +924,71 @@ __device__ __forceinline__ void step_scan(const KgmtDev& d, int4 pk, int* sPfx, 
     *jGoal = __builtin_amdgcn_readfirstlane(min(min(sRed[1][0], sRed[1][1]), min(sRed[1][2], sRed[1][3])));
 }
 
+// step_scan for a sharded rank: t-1's packed count words of every rank's blocks
+// (the exchange's count field, up to kMaxShardStepBlocks), `per` consecutive blocks
+// per thread.  Pass 1 keeps each thread's local prefix in LDS, pass 2 adds the
+// thread's base; the lowest goal child is found as in step_scan.
+__device__ __forceinline__ void step_scan_sh(const KgmtDev& d, const SBMP_GAS int* cnt, int* sPfx,
+                                             int (*sRed)[kBlock / kWave], int* A, int* jGoal) {
+    constexpr int kV = kMaxShardStepBlocks / (4 * kBlock);   // int4 loads per thread at most
+    const int tid = threadIdx.x;
+    const int lane = tid & (kWave - 1);
+    const int wave = tid >> 6;
+    const int nb4 = (d.nBlocks + 3) & ~3;
+    const int per = ((nb4 + 4 * kBlock - 1) / (4 * kBlock)) * 4;   // multiple of 4, <= 4 kV
+    const int g0 = tid * per;
+    int4 v[kV];
+#pragma unroll
+    for (int i = 0; i < kV; ++i)   // every load in flight before the first use
+        if (4 * i < per) v[i] = *reinterpret_cast<const SBMP_GAS int4*>(cnt + min(g0 + 4 * i, nb4 - 4));
+    int run = 0, gloc = kNoGoalIdx;
+#pragma unroll
+    for (int i = 0; i < kV; ++i) {
+        if (4 * i < per) {
+            const int e[4] = {v[i].x, v[i].y, v[i].z, v[i].w};
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const int g = g0 + 4 * i + k;
+                int c, gl;
+                step_unpack(g < nb4 ? e[k] : 0, &c, &gl);
+                if (g <= d.nBlocks) sPfx[g] = run;
+                if (gl >= 0 && gloc == kNoGoalIdx) gloc = run + gl;   // prefixes grow with g
+                run += c;
+            }
+        }
+    }
+    const int incl = wave_incl_sum(run);
+    if (lane == kWave - 1) sRed[0][wave] = incl;
+    __syncthreads();
+    int base = incl - run;
+    base += (wave > 0 ? sRed[0][0] : 0) + (wave > 1 ? sRed[0][1] : 0) + (wave > 2 ? sRed[0][2] : 0);
+    *A = __builtin_amdgcn_readfirstlane(sRed[0][0] + sRed[0][1] + sRed[0][2] + sRed[0][3]);
+    for (int g = g0; g < g0 + per && g <= d.nBlocks; ++g) sPfx[g] += base;
+    if (tid == 0 && g0 + per * kBlock <= d.nBlocks) sPfx[d.nBlocks] = *A;   // past every thread's range
+    int gmin = (gloc != kNoGoalIdx) ? base + gloc : kNoGoalIdx;
+    gmin = first_lane_value(gmin != kNoGoalIdx, gmin, kNoGoalIdx);
+    if (lane == 0) sRed[1][wave] = gmin;
+    __syncthreads();
+    *jGoal = __builtin_amdgcn_readfirstlane(min(min(sRed[1][0], sRed[1][1]), min(sRed[1][2], sRed[1][3])));
+}
+
+// The list entry (state, ctrl, cost) of row j of t-1's flagged children, given the
+// block lo holding it: a single rank's own compacted list, or on a sharded rank the
+// owner's (rank lo mod P, owned block lo / P) through its record buffer.
+template <bool SH>
+__device__ __forceinline__ const SBMP_GAS float4* list_entry(const KgmtDev& d, int pp, int lo, int i) {
+    if constexpr (SH)
+        return G(d.recPeer[lo % d.nranks]) +
+               ((size_t)pp * d.recCap + (size_t)(lo / d.nranks) * kBlock + i) * kStepEntry;
+    else
+        return G(d.stepList) + ((size_t)pp * d.nBlocks * kBlock + (size_t)lo * kBlock + i) * kStepEntry;
+}
+template <bool SH>
+__device__ __forceinline__ float4 list_load(const SBMP_GAS float4* p) {
+    if constexpr (SH) return load_record_g(p);   // peer memory, or lines cached two iterations ago
+    else return *p;
+}
+
 // Plan scalars of iteration t from t-1's control block and the scan (KGMT.cu:118,
 // 139-188,249-259); every workgroup derives the same values.
 struct StepPlan {
@@ -946,6 +1027,7 @@ __device__ __forceinline__ StepPlan step_plan(const KgmtDev& d, int t, int expan
 // Workgroup 0 of k_step(t): tables of t (R1 deltas folded, R2New merged into R2Avail
 // = the snapshot, R1Cov), scores (updateR1, KGMT.cu:485-538, CUB order D8), ctrl[t];
 // scores and snapshot published as 8-B words tagged with t.
+template <bool SH>
 __device__ __forceinline__ void step_planner(const KgmtDev& d, int t, int expand, int* sPfx,
                                              int (*sRed)[kBlock / kWave], int* sCovInc, float* sPart) {
     constexpr int kW = kMaxR2Words / kBlock;
@@ -958,13 +1040,16 @@ __device__ __forceinline__ void step_planner(const KgmtDev& d, int t, int expand
     const bool tl = d.timelineFin && t == d.timelineIter && tid == 0;   // diagnostics: entry, publish
     if (tl) G(d.timelineFin)[0] = (long long)__builtin_amdgcn_s_memrealtime();
     // every input at entry
-    const int4 pk = *reinterpret_cast<const SBMP_GAS int4*>(G(d.stepCnt) + (size_t)pp * kMaxStepBlocks + tid * 4);
+    int4 pk = make_int4(0, 0, 0, 0);
+    if constexpr (!SH) pk = *reinterpret_cast<const SBMP_GAS int4*>(G(d.stepCnt) + (size_t)pp * kMaxStepBlocks + tid * 4);
     const IterCtrl pc = G(d.ctrl)[t - 1];
     const int goalIdx = G(d.status)->goalIdx;
     const SBMP_GAS int* tabPrev = G(d.R1) + (size_t)pp * 5 * d.nR1;
     int r1 = tabPrev[cell], r1a = tabPrev[d.nR1 + cell], r1v = tabPrev[2 * d.nR1 + cell],
         r1i = tabPrev[3 * d.nR1 + cell], r1c = tabPrev[4 * d.nR1 + cell];
-    const SBMP_GAS unsigned long long* deltaPrev = G(d.stepDelta) + (size_t)((t - 1) % 3) * kDeltaReps * d.nR1;
+    // sharded: the exchange's sum over ranks; else ring (t - 1) % 3
+    const SBMP_GAS unsigned long long* deltaPrev =
+        SH ? G(d.stepXr) : G(d.stepDelta) + (size_t)((t - 1) % 3) * kDeltaReps * d.nR1;
     unsigned long long dl = 0ull;   // replicas: carry-free sums
 #pragma unroll
     for (int r = 0; r < kDeltaReps; ++r) dl += deltaPrev[(size_t)r * d.nR1 + cell];
@@ -978,8 +1063,27 @@ __device__ __forceinline__ void step_planner(const KgmtDev& d, int t, int expand
         newW[j] = 0u;
     }
     // the R2New replicas: n <= 8 (two words per thread) with all 16 loads in flight;
-    // larger grids one word at a time (8 VGPRs live: all 64 at once would spill)
-    if (nW <= 2 * kBlock) {
+    // larger grids one word at a time (8 VGPRs live: all 64 at once would spill).
+    // Sharded: the exchange's bytes (a sum over ranks of 0/1 per cell), 32 per word.
+    if constexpr (SH) {
+        const SBMP_GAS uint8_t* nbp = reinterpret_cast<const SBMP_GAS uint8_t*>(G(d.stepXr) + d.xNewOff);
+#pragma unroll
+        for (int j = 0; j < kW; ++j) {
+            if (j * kBlock < nW) {   // uniform
+                const int w = min(tid + j * kBlock, nW - 1);
+                const uint4 b0 = reinterpret_cast<const SBMP_GAS uint4*>(nbp + 32 * (size_t)w)[0];
+                const uint4 b1 = reinterpret_cast<const SBMP_GAS uint4*>(nbp + 32 * (size_t)w)[1];
+                const uint32_t qv[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+                uint32_t nw = 0u;
+#pragma unroll
+                for (int k = 0; k < 8; ++k) {   // nonzero bytes -> 4 bits (sums <= nranks never carry)
+                    const uint32_t hi = (((qv[k] & 0x7f7f7f7fu) + 0x7f7f7f7fu) | qv[k]) & 0x80808080u;
+                    nw |= ((((hi >> 7) * 0x00204081u) >> 21) & 0xfu) << (4 * k);
+                }
+                newW[j] = nw;
+            }
+        }
+    } else if (nW <= 2 * kBlock) {
         newW[0] = merge_new(newPrev, nW, min(tid, nW - 1));
         newW[1] = merge_new(newPrev, nW, min(tid + kBlock, nW - 1));
     } else {
@@ -989,7 +1093,8 @@ __device__ __forceinline__ void step_planner(const KgmtDev& d, int t, int expand
     }
     for (int i = tid; i < d.nR1; i += kBlock) sCovInc[i] = 0;
     int A, jGoal;
-    step_scan(d, pk, sPfx, sRed, &A, &jGoal);
+    if constexpr (SH) step_scan_sh(d, reinterpret_cast<const SBMP_GAS int*>(G(d.stepXr) + d.xCntOff), sPfx, sRed, &A, &jGoal);
+    else step_scan(d, pk, sPfx, sRed, &A, &jGoal);
     const StepPlan q = step_plan(d, t, expand, pc, goalIdx, A, jGoal);
     SBMP_GAS int* tabCur = G(d.R1) + (size_t)cp * 5 * d.nR1;
     if (!q.ranPrev) {   // t-1 did not run: the loop has ended; carry the tables forward
@@ -1081,7 +1186,11 @@ __device__ __forceinline__ void step_planner(const KgmtDev& d, int t, int expand
         const int w = tid + j * kBlock;
         if (j * kBlock < nW && w < nW) G(d.R2Avail)[(size_t)cp * nW + w] = snapW[j];
     }
-    {   // ring (t+1) % 3, last read by k_step(t-1): zero for k_step(t+1)
+    if constexpr (SH) {   // send parity (t+1) & 1, last read by exchange t-1: zero for k_step(t+1)
+        SBMP_GAS unsigned long long* zx = G(d.stepXs[(t + 1) & 1]);
+        for (int i = tid; i < kDeltaReps * d.nR1; i += kBlock) zx[i] = 0ull;
+        for (int i = tid; i < d.nR2 / 8; i += kBlock) zx[d.xNewOff + i] = 0ull;   // R2New bytes (count words: owner-written)
+    } else {   // ring (t+1) % 3, last read by k_step(t-1): zero for k_step(t+1)
         SBMP_GAS unsigned long long* zd = G(d.stepDelta) + (size_t)((t + 1) % 3) * kDeltaReps * d.nR1;
         for (int i = tid; i < kDeltaReps * d.nR1; i += kBlock) zd[i] = 0ull;
         SBMP_GAS uint32_t* zn = G(d.stepR2New) + (size_t)((t + 1) % 3) * kNewReps * nW;
@@ -1110,13 +1219,12 @@ __device__ __forceinline__ void step_planner(const KgmtDev& d, int t, int expand
     // workgroup is idle.
     if (t > 1 && A <= kPlannerInsertMax) {
         const int n = min(q.nIns, d.M - q.tsPrev);   // D13: the reference writes past M
-        const SBMP_GAS float4* listPrev = G(d.stepList) + (size_t)pp * d.nBlocks * kBlock * kStepEntry;
         // list entry of row j: block lo with sPfx[lo] <= j < sPfx[lo + 1]
         auto entry = [&](int j) {
             int lo = 0;
-            for (int step = kMaxStepBlocks / 2; step > 0; step >>= 1)
+            for (int step = (SH ? kMaxShardStepBlocks : kMaxStepBlocks) / 2; step > 0; step >>= 1)
                 if (lo + step < d.nBlocks && sPfx[lo + step] <= j) lo += step;
-            return listPrev + ((size_t)lo * kBlock + (j - sPfx[lo])) * kStepEntry;
+            return list_entry<SH>(d, pp, lo, j - sPfx[lo]);
         };
         auto put = [&](int j, float4 s4, float4 u4, float c) {
             const int dst = q.tsPrev + j;
@@ -1128,8 +1236,9 @@ __device__ __forceinline__ void step_planner(const KgmtDev& d, int t, int expand
             const int j1 = j0 + kBlock;
             const SBMP_GAS float4* e0 = entry(j0);
             const SBMP_GAS float4* e1 = entry(min(j1, n - 1));
-            const float4 s0 = e0[0], u0 = e0[1], s1 = e1[0], u1 = e1[1];
-            const float c0 = e0[2].x, c1 = e1[2].x;
+            const float4 s0 = list_load<SH>(e0), u0 = list_load<SH>(e0 + 1), s1 = list_load<SH>(e1),
+                         u1 = list_load<SH>(e1 + 1);
+            const float c0 = list_load<SH>(e0 + 2).x, c1 = list_load<SH>(e1 + 2).x;
             put(j0, s0, u0, c0);
             if (j1 < n) put(j1, s1, u1, c1);
         }
@@ -1147,13 +1256,16 @@ __device__ __forceinline__ void step_planner(const KgmtDev& d, int t, int expand
 //              LDS staging and no barrier; stores overlap that round trip;
 //   epilogue   one barrier: wave counts -> list positions, the R1 / R2New flushes and
 //              the block's packed count.
-template <int AGENT, int OBS>
+// SH: a sharded rank: workgroup b expands owned block rank + P b; the
+// counts, R1 deltas and R2New of t-1 come from the exchange (stepXr), this launch's
+// go to stepXs[t & 1]; the flagged children's lists are the record buffers, and
+// workgroup b inserts t-1's children of blocks b P .. b P + P - 1 (one of each rank).
+template <int AGENT, int OBS, bool SH>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) void k_step(
     const KgmtDev* __restrict__ dp, int t, int expand, long long* tlBase) {
     const KgmtDev& d = *dp;
-    extern __shared__ float4 sDyn[];   // [LDS obstacles][prefix: nBlocks + 1 ints]
+    extern __shared__ float4 sDyn[];   // [LDS obstacles][prefix: nBlocks + 1 ints][R2New bits: nR2 / 32]
     __shared__ int sR1P[kMaxR1];
-    __shared__ uint32_t sNew[kMaxR2Words];
     __shared__ int sWaveCnt[kBlock / kWave];
     __shared__ int sWaveGoal[kBlock / kWave];
     __shared__ int sRed[2][kBlock / kWave];
@@ -1163,16 +1275,18 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) voi
     constexpr bool kLdsObs = (OBS == kObsLds || OBS == kObsLds4);
     constexpr int kRegObs = obs_in_registers(OBS);
     int* const sPfx = reinterpret_cast<int*>(sDyn + (kLdsObs ? d.nObs : 0));
+    uint32_t* const sNew = reinterpret_cast<uint32_t*>(sPfx + d.nBlocks + 1);
     if (blockIdx.x == 0) {
-        step_planner(d, t, expand, sPfx, sRed, sCovInc, sPart);
+        step_planner<SH>(d, t, expand, sPfx, sRed, sCovInc, sPart);
         return;
     }
     float4* const sObs = sDyn;
     const int tid = threadIdx.x;
     const int lane = tid & (kWave - 1);
     const int wave = tid >> 6;
-    const int b = (int)blockIdx.x - 1;   // this workgroup's 256-slot block
-    const int slot = b * kBlock + tid;
+    const int b = (int)blockIdx.x - 1;                // this workgroup's 256-slot block (owned index)
+    const int gb = SH ? d.rank + d.nranks * b : b;   // global block
+    const int slot = gb * kBlock + tid;
     const int nW = d.nR2 >> 5;
     const int pp = (t - 1) & 1, cp = t & 1;
     const SBMP_GAS unsigned long long* const pubCur = G(d.stepPub) + (size_t)cp * (d.nR1 + nW);
@@ -1201,7 +1315,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) voi
 
     // ---- loads that depend on nothing else (the control block as a plain load: a
     // waiting scalar load would serialise behind the scan)
-    const int4 pk = *reinterpret_cast<const SBMP_GAS int4*>(cntP + (size_t)pp * kMaxStepBlocks + tid * 4);
+    int4 pk = make_int4(0, 0, 0, 0);
+    if constexpr (!SH) pk = *reinterpret_cast<const SBMP_GAS int4*>(cntP + (size_t)pp * kMaxStepBlocks + tid * 4);
     const IterCtrl pc = ctrlP[t - 1];
     const int goalIdx = statusP->goalIdx;
     const uint4 ra = rngAP[slot];
@@ -1217,7 +1332,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) voi
     ChildCtl ctl = draw_controls<AGENT>(rs, d);
     asm volatile("" : "+v"(ctl.a), "+v"(ctl.steer), "+v"(ctl.dur), "+v"(ctl.dt), "+v"(ctl.tanS));
     int A, jGoal;
-    step_scan(d, pk, sPfx, sRed, &A, &jGoal);
+    if constexpr (SH) step_scan_sh(d, reinterpret_cast<const SBMP_GAS int*>(G(d.stepXr) + d.xCntOff), sPfx, sRed, &A, &jGoal);
+    else step_scan(d, pk, sPfx, sRed, &A, &jGoal);
     SBMP_STAMP(1);
     // the control block and the goal index were loaded per lane (vector loads do not
     // wait behind the scan's scalar work); the plan is wave-uniform, so scalar code
@@ -1238,25 +1354,32 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) voi
         if (wbase + kWave <= cleared) word = 0ull;
         else if (wbase < cleared) word = oldWord & ~((1ull << (cleared - wbase)) - 1ull);
     }
-    const bool doExpand = q.executes && b * kBlock < q.H;
+    const bool doExpand = q.executes && gb * kBlock < q.H;
     // ---- insert t-1: this block's flagged children (rows treeSize(t-1) + prefix +
     // index).  Each entry carries its cost, so this is one load and three stores; an
     // expanding block issues it right behind its parent loads (one round trip).
-    const int myPrev = sPfx[b + 1] - sPfx[b];
     const bool selfInsert = A > kPlannerInsertMax;   // else the planner workgroup inserts
-    auto insert_prev = [&]() {
-        if (t > 1 && selfInsert && tid < myPrev) {
-            const int j = sPfx[b] + tid;
+    auto insert_block = [&](int lo) {   // t-1's flagged children of global block lo
+        if (tid < sPfx[lo + 1] - sPfx[lo]) {
+            const int j = sPfx[lo] + tid;
             const int dst = q.tsPrev + j;
             if (j < q.nIns && dst < d.M) {   // D13: the reference writes past M here
-                const SBMP_GAS float4* e =
-                    G(d.stepList) + ((size_t)pp * d.nBlocks * kBlock + (size_t)b * kBlock + tid) * kStepEntry;
-                const float4 s4 = e[0];
-                const float4 u4 = e[1];
-                const float4 m4 = e[2];
+                const SBMP_GAS float4* e = list_entry<SH>(d, pp, lo, tid);
+                const float4 s4 = list_load<SH>(e);
+                const float4 u4 = list_load<SH>(e + 1);
+                const float4 m4 = list_load<SH>(e + 2);
                 G(d.treeState)[dst] = s4;
                 G(d.treeCtrl)[dst] = make_float4(u4.x, u4.y, u4.z, m4.x);   // cost = parent's + duration (KGMT.cu:631-633)
                 G(d.treeParent)[dst] = __float_as_int(u4.w);
+            }
+        }
+    };
+    auto insert_prev = [&]() {
+        if (t > 1 && selfInsert) {
+            if constexpr (SH) {   // every rank holds the whole tree: blocks b P .. b P + P - 1
+                for (int r = 0; r < d.nranks; ++r) insert_block(b * d.nranks + r);
+            } else {
+                insert_block(b);
             }
         }
     };
@@ -1284,7 +1407,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) voi
         const int jA = __builtin_amdgcn_readlane(j, (int)__builtin_ctzll(need));
         const int jB = __builtin_amdgcn_readlane(j, 63 - (int)__builtin_clzll(need));
         int lo = 0;
-        if (jB - jA <= 1) {
+        if (jB - jA <= 1 && d.nBlocks <= kMaxStepBlocks) {   // two 32-ary levels cover 1,024 blocks
             const int jj = (lane < 32) ? jA : jB;
             const int sub = lane & 31;
             int idx = sub * 32;
@@ -1302,13 +1425,20 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) voi
             }
         }
         if (fromList) {
-            src = G(d.stepList) + ((size_t)pp * d.nBlocks * kBlock + (size_t)lo * kBlock + (j - sPfx[lo])) * kStepEntry;
+            src = list_entry<SH>(d, pp, lo, j - sPfx[lo]);
             srcCost = reinterpret_cast<const SBMP_GAS float*>(src + 2);
         }
     }
     // Parent and obstacles are issued back to back and waited for together.
-    const float4 p = *src;
-    const float parentCost = *srcCost;
+    float4 p;
+    float parentCost;
+    if (SH && fromList) {   // the owner's list: system-scope loads
+        p = load_record_g(src);
+        parentCost = load_record_g(src + 2).x;
+    } else {
+        p = *src;
+        parentCost = *srcCost;
+    }
     float4 ro[kRegObs > 0 ? kRegObs : 1];
 #pragma unroll
     for (int i = 0; i < kRegObs; ++i) ro[i] = G(d.obstacles)[i];
@@ -1432,25 +1562,44 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) voi
     const int c0 = sWaveCnt[0], c1 = sWaveCnt[1], c2 = sWaveCnt[2], c3 = sWaveCnt[3];
     const int waveOff = (wave > 0 ? c0 : 0) + (wave > 1 ? c1 : 0) + (wave > 2 ? c2 : 0);
     if (flagged) {
-        SBMP_GAS float4* e = G(d.stepList) + ((size_t)cp * d.nBlocks * kBlock + (size_t)b * kBlock + waveOff + idxW) * kStepEntry;
-        e[0] = cs;
-        e[1] = cc;
-        e[2] = make_float4(cost, 0.0f, 0.0f, 0.0f);
+        if constexpr (SH) {   // this rank's list of owned block b, written through for the peers
+            SBMP_GAS float4* e = G(d.recOut) + ((size_t)cp * d.recCap + (size_t)b * kBlock + waveOff + idxW) * kStepEntry;
+            store_record_g(e, cs);
+            store_record_g(e + 1, cc);
+            store_record_g(e + 2, make_float4(cost, 0.0f, 0.0f, 0.0f));
+        } else {
+            SBMP_GAS float4* e =
+                G(d.stepList) + ((size_t)cp * d.nBlocks * kBlock + (size_t)b * kBlock + waveOff + idxW) * kStepEntry;
+            e[0] = cs;
+            e[1] = cc;
+            e[2] = make_float4(cost, 0.0f, 0.0f, 0.0f);
+        }
     }
     {   // one 64-bit atomic per touched cell, into this workgroup's replica
         SBMP_GAS unsigned long long* const rep =
-            G(d.stepDelta) + (size_t)(t % 3) * kDeltaReps * d.nR1 + (size_t)(b % kDeltaReps) * d.nR1;
+            (SH ? G(d.stepXs[cp]) : G(d.stepDelta) + (size_t)(t % 3) * kDeltaReps * d.nR1) + (size_t)(b % kDeltaReps) * d.nR1;
         const int v = sR1P[tid];   // nR1 == kBlock
         if (v)
             __hip_atomic_fetch_add(rep + tid, (unsigned long long)(v & 0xffff) | ((unsigned long long)(v >> 16) << 32),
                                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    // replicas: a device atomic on one word serialises (~11 ns each); in the early
-    // iterations most blocks set the same few words, so each replica sees 1/kNewReps
-    SBMP_GAS uint32_t* const newCur = G(d.stepR2New) + ((size_t)(t % 3) * kNewReps + (size_t)(b % kNewReps)) * nW;
-    for (int i = tid; i < nW; i += kBlock) {
-        const uint32_t w = sNew[i];
-        if (w) __hip_atomic_fetch_or(newCur + i, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if constexpr (SH) {   // R2New as bytes of the exchange (a sum over ranks), one store per cell the block saw
+        SBMP_GAS uint8_t* const nb = reinterpret_cast<SBMP_GAS uint8_t*>(G(d.stepXs[cp]) + d.xNewOff);
+        for (int i = tid; i < nW; i += kBlock) {
+            uint32_t w = sNew[i];
+            while (w) {
+                nb[32 * i + __builtin_ctz(w)] = 1;
+                w &= w - 1u;
+            }
+        }
+    } else {
+        // replicas: a device atomic on one word serialises (~11 ns each); in the early
+        // iterations most blocks set the same few words, so each replica sees 1/kNewReps
+        SBMP_GAS uint32_t* const newCur = G(d.stepR2New) + ((size_t)(t % 3) * kNewReps + (size_t)(b % kNewReps)) * nW;
+        for (int i = tid; i < nW; i += kBlock) {
+            const uint32_t w = sNew[i];
+            if (w) __hip_atomic_fetch_or(newCur + i, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
     }
     if (tid == 0) {   // the block's flagged count and its lowest goal child (in-block index)
         const int g0 = sWaveGoal[0], g1 = sWaveGoal[1], g2 = sWaveGoal[2], g3 = sWaveGoal[3];
@@ -1459,7 +1608,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) voi
         if (g2 != kNoGoalIdx) gmin = c0 + c1 + g2;
         if (g1 != kNoGoalIdx) gmin = c0 + g1;
         if (g0 != kNoGoalIdx) gmin = g0;
-        G(d.stepCnt)[(size_t)cp * kMaxStepBlocks + b] = (c0 + c1 + c2 + c3) | ((gmin == kNoGoalIdx ? 0 : gmin + 1) << 16);
+        const int cw = (c0 + c1 + c2 + c3) | ((gmin == kNoGoalIdx ? 0 : gmin + 1) << 16);
+        if constexpr (SH) reinterpret_cast<SBMP_GAS int*>(G(d.stepXs[cp]) + d.xCntOff)[gb] = cw;
+        else G(d.stepCnt)[(size_t)cp * kMaxStepBlocks + b] = cw;
     }
     SBMP_STAMP(6);
     if (tl) {
@@ -1644,34 +1795,43 @@ void launch_expand(const KgmtDev& d, int t, int agent, int blocks, int variant, 
     else launch_expand_agent<1>(d, t, blocks, variant, s, tm);
 }
 
+template <int AGENT, bool SH>
+static void launch_step_form(const KgmtDev& d, int t, int expand, int variant, hipStream_t s,
+                             const KernelTiming& tm) {
+    // dynamic LDS: [LDS obstacles][block prefix: nBlocks + 1 ints][R2New bits: nR2 / 32 words]
+    const size_t pfx = sizeof(int) * ((size_t)d.nBlocks + 1) + sizeof(uint32_t) * (size_t)(d.nR2 / 32);
+    const size_t shm = sizeof(float4) * (size_t)d.nObs + pfx;   // LDS obstacle forms
+    const int blocks = SH ? d.nBlocks / d.nranks : d.nBlocks;
+    const dim3 grid(1 + blocks), block(kBlock);   // workgroup 0 plans, 1.. expand
+    long long* const tlBase = (!SH && d.timeline && t == d.timelineIter && expand) ? d.timeline : nullptr;
+    if (d.gridStart) {
+        launch(k_step<AGENT, kObsGrid, SH>, grid, block, pfx, s, tm, d.devSelf, t, expand, tlBase);
+    } else if (d.nObs > kMaxLdsObs) {
+        launch(k_step<AGENT, kObsGlobal, SH>, grid, block, pfx, s, tm, d.devSelf, t, expand, tlBase);
+    } else if (d.nObs <= kMaxRegObs && (variant == 0 || variant == 3)) {
+        switch (d.nObs) {
+            case 0: launch(k_step<AGENT, kObsReg + 0, SH>, grid, block, pfx, s, tm, d.devSelf, t, expand, tlBase); break;
+            case 1: launch(k_step<AGENT, kObsReg + 1, SH>, grid, block, pfx, s, tm, d.devSelf, t, expand, tlBase); break;
+            case 2: launch(k_step<AGENT, kObsReg + 2, SH>, grid, block, pfx, s, tm, d.devSelf, t, expand, tlBase); break;
+            case 3: launch(k_step<AGENT, kObsReg + 3, SH>, grid, block, pfx, s, tm, d.devSelf, t, expand, tlBase); break;
+            case 4: launch(k_step<AGENT, kObsReg + 4, SH>, grid, block, pfx, s, tm, d.devSelf, t, expand, tlBase); break;
+            case 5: launch(k_step<AGENT, kObsReg + 5, SH>, grid, block, pfx, s, tm, d.devSelf, t, expand, tlBase); break;
+            case 6: launch(k_step<AGENT, kObsReg + 6, SH>, grid, block, pfx, s, tm, d.devSelf, t, expand, tlBase); break;
+            case 7: launch(k_step<AGENT, kObsReg + 7, SH>, grid, block, pfx, s, tm, d.devSelf, t, expand, tlBase); break;
+            default: launch(k_step<AGENT, kObsReg + 8, SH>, grid, block, pfx, s, tm, d.devSelf, t, expand, tlBase); break;
+        }
+    } else if (variant == 2) {
+        launch(k_step<AGENT, kObsLds4, SH>, grid, block, shm, s, tm, d.devSelf, t, expand, tlBase);
+    } else {
+        launch(k_step<AGENT, kObsLds, SH>, grid, block, shm, s, tm, d.devSelf, t, expand, tlBase);
+    }
+}
+
 template <int AGENT>
 static void launch_step_agent(const KgmtDev& d, int t, int expand, int variant, hipStream_t s,
                               const KernelTiming& tm) {
-    const size_t pfx = sizeof(int) * ((size_t)d.nBlocks + 1);
-    const size_t shm = sizeof(float4) * (size_t)d.nObs + pfx;   // LDS obstacle forms
-    const dim3 grid(1 + d.nBlocks), block(kBlock);   // workgroup 0 plans, 1.. expand
-    long long* const tlBase = (d.timeline && t == d.timelineIter && expand) ? d.timeline : nullptr;
-    if (d.gridStart) {
-        launch(k_step<AGENT, kObsGrid>, grid, block, pfx, s, tm, d.devSelf, t, expand, tlBase);
-    } else if (d.nObs > kMaxLdsObs) {
-        launch(k_step<AGENT, kObsGlobal>, grid, block, pfx, s, tm, d.devSelf, t, expand, tlBase);
-    } else if (d.nObs <= kMaxRegObs && (variant == 0 || variant == 3)) {
-        switch (d.nObs) {
-            case 0: launch(k_step<AGENT, kObsReg + 0>, grid, block, pfx, s, tm, d.devSelf, t, expand, tlBase); break;
-            case 1: launch(k_step<AGENT, kObsReg + 1>, grid, block, pfx, s, tm, d.devSelf, t, expand, tlBase); break;
-            case 2: launch(k_step<AGENT, kObsReg + 2>, grid, block, pfx, s, tm, d.devSelf, t, expand, tlBase); break;
-            case 3: launch(k_step<AGENT, kObsReg + 3>, grid, block, pfx, s, tm, d.devSelf, t, expand, tlBase); break;
-            case 4: launch(k_step<AGENT, kObsReg + 4>, grid, block, pfx, s, tm, d.devSelf, t, expand, tlBase); break;
-            case 5: launch(k_step<AGENT, kObsReg + 5>, grid, block, pfx, s, tm, d.devSelf, t, expand, tlBase); break;
-            case 6: launch(k_step<AGENT, kObsReg + 6>, grid, block, pfx, s, tm, d.devSelf, t, expand, tlBase); break;
-            case 7: launch(k_step<AGENT, kObsReg + 7>, grid, block, pfx, s, tm, d.devSelf, t, expand, tlBase); break;
-            default: launch(k_step<AGENT, kObsReg + 8>, grid, block, pfx, s, tm, d.devSelf, t, expand, tlBase); break;
-        }
-    } else if (variant == 2) {
-        launch(k_step<AGENT, kObsLds4>, grid, block, shm, s, tm, d.devSelf, t, expand, tlBase);
-    } else {
-        launch(k_step<AGENT, kObsLds>, grid, block, shm, s, tm, d.devSelf, t, expand, tlBase);
-    }
+    if (d.sharded) launch_step_form<AGENT, true>(d, t, expand, variant, s, tm);
+    else launch_step_form<AGENT, false>(d, t, expand, variant, s, tm);
 }
 
 void launch_step(const KgmtDev& d, int t, int expand, int agent, int variant, hipStream_t s,

@@ -186,12 +186,21 @@ KgmtPlanner::KgmtPlanner(const sbmp_kgmt_params& p, int nranks, int rank, Exchan
         // Sharded: [R1 delta replicas | block prefixes pfx | rank totals | R2New bytes]
         //          is all-reduced; block counts and GNew words are the owner's alone
         //          (a separate local buffer), since the inserts are record-driven.
+        // Sharded k_step (one launch per iteration): [R1 delta replicas | packed block
+        //          count words (nBlocks, int4-readable) | R2New bytes], two send parities.
         const bool sharded = nranks > 1 || ex;
+        const char* sv = std::getenv("SBMP_STEP");
+        shStep_ = sharded && d.nBlocks <= kMaxShardStepBlocks && !(sv && atoi(sv) == 0);
         const size_t dWords = round_up((long long)kDeltaReps * d.nR1, 2);
         const size_t bcWords = round_up(d.nBlocks, 4) / 2, r2Words = round_up(d.nR2, 16) / 8;
         const size_t pfxWords = round_up(d.nBlocks + 1, 4) / 2, totWords = kMaxRanks / 2;
         unsigned long long* local = nullptr;
-        if (sharded) {
+        if (shStep_) {
+            xWords_ = dWords + bcWords + r2Words;
+            local = alloc<unsigned long long>(bcWords + (size_t)nWords);
+            localWords_ = bcWords + (size_t)nWords;
+            local_ = local;
+        } else if (sharded) {
             xWords_ = dWords + pfxWords + totWords + r2Words;
             local = alloc<unsigned long long>(bcWords + (size_t)nWords);
             localWords_ = bcWords + (size_t)nWords;
@@ -200,7 +209,13 @@ KgmtPlanner::KgmtPlanner(const sbmp_kgmt_params& p, int nranks, int rank, Exchan
             xWords_ = dWords + bcWords + (size_t)nWords + r2Words;
         }
         xSend_ = alloc<unsigned long long>(xWords_);
+        xSendOdd_ = shStep_ ? alloc<unsigned long long>(xWords_) : xSend_;
         xRecv_ = sharded ? alloc<unsigned long long>(xWords_) : xSend_;
+        d.stepXs[0] = shStep_ ? xSend_ : nullptr;
+        d.stepXs[1] = shStep_ ? xSendOdd_ : nullptr;
+        d.stepXr = shStep_ ? xRecv_ : nullptr;
+        d.xCntOff = (int)dWords;
+        d.xNewOff = (int)(dWords + bcWords);
         int* bc = reinterpret_cast<int*>(sharded ? local : xSend_ + dWords);
         unsigned long long* gn = sharded ? local + bcWords : xSend_ + dWords + bcWords;
         d.blockCountOut = bc;
@@ -233,7 +248,7 @@ KgmtPlanner::KgmtPlanner(const sbmp_kgmt_params& p, int nranks, int rank, Exchan
     d.stepMode = 0;
     {
         const char* v = getenv("SBMP_STEP");
-        if (!d.sharded && d.nBlocks <= kMaxStepBlocks && !(v && atoi(v) == 0)) d.stepMode = 1;
+        if ((!d.sharded && d.nBlocks <= kMaxStepBlocks && !(v && atoi(v) == 0)) || shStep_) d.stepMode = 1;
     }
     d.stepCnt = nullptr;
     d.stepPub = nullptr;
@@ -241,11 +256,13 @@ KgmtPlanner::KgmtPlanner(const sbmp_kgmt_params& p, int nranks, int rank, Exchan
     d.stepDelta = nullptr;
     d.stepR2New = nullptr;
     if (d.stepMode) {
-        d.stepCnt = alloc<int>((size_t)2 * kMaxStepBlocks);
         d.stepPub = alloc<unsigned long long>((size_t)2 * (d.nR1 + d.nR2 / 32));
-        d.stepList = alloc<float4>((size_t)2 * d.nBlocks * kBlock * kStepEntry);
-        d.stepDelta = alloc<unsigned long long>((size_t)3 * kDeltaReps * d.nR1);
-        d.stepR2New = alloc<uint32_t>((size_t)3 * kNewReps * (d.nR2 / 32));
+        if (!d.sharded) {   // a sharded rank's counts, deltas and R2New travel in the exchange, its lists in recOut
+            d.stepCnt = alloc<int>((size_t)2 * kMaxStepBlocks);
+            d.stepList = alloc<float4>((size_t)2 * d.nBlocks * kBlock * kStepEntry);
+            d.stepDelta = alloc<unsigned long long>((size_t)3 * kDeltaReps * d.nR1);
+            d.stepR2New = alloc<uint32_t>((size_t)3 * kNewReps * (d.nR2 / 32));
+        }
         dDev_ = alloc<KgmtDev>(1);
         SBMP_HIP(hipHostMalloc(reinterpret_cast<void**>(&dStage_), sizeof(KgmtDev), hipHostMallocDefault));
     }
@@ -335,13 +352,14 @@ void KgmtPlanner::begin(const float* initial, const float* goal, const float* d_
     SBMP_HIP(hipMemsetAsync(d.treeCtrl, 0, sizeof(float4) * d.M, s));
     launch_fill_i32(d.treeParent, -1, d.M, s);
     SBMP_HIP(hipMemsetAsync(xSend_, 0, sizeof(unsigned long long) * xWords_, s));
+    if (xSendOdd_ != xSend_) SBMP_HIP(hipMemsetAsync(xSendOdd_, 0, sizeof(unsigned long long) * xWords_, s));
     if (local_) SBMP_HIP(hipMemsetAsync(local_, 0, sizeof(unsigned long long) * localWords_, s));
     if (xRecv_ != xSend_) SBMP_HIP(hipMemsetAsync(xRecv_, 0, sizeof(unsigned long long) * xWords_, s));
     SBMP_HIP(hipMemsetAsync(d.R1, 0, sizeof(int) * 2 * 5 * d.nR1, s));   // both parities
     SBMP_HIP(hipMemsetAsync(d.R2Avail, 0, sizeof(uint32_t) * 2 * (d.nR2 / 32), s));
-    if (d.stepMode) {
+    if (d.stepMode) SBMP_HIP(hipMemsetAsync(d.stepPub, 0, sizeof(unsigned long long) * 2 * (d.nR1 + d.nR2 / 32), s));
+    if (d.stepMode && !d.sharded) {
         SBMP_HIP(hipMemsetAsync(d.stepCnt, 0, sizeof(int) * 2 * kMaxStepBlocks, s));
-        SBMP_HIP(hipMemsetAsync(d.stepPub, 0, sizeof(unsigned long long) * 2 * (d.nR1 + d.nR2 / 32), s));
         SBMP_HIP(hipMemsetAsync(d.stepDelta, 0, sizeof(unsigned long long) * 3 * kDeltaReps * d.nR1, s));
         SBMP_HIP(hipMemsetAsync(d.stepR2New, 0, sizeof(uint32_t) * 3 * kNewReps * (d.nR2 / 32), s));
     }
@@ -435,16 +453,15 @@ void KgmtPlanner::enqueue(int iterations) {
         const int t = take_iteration();
         if (t == 0) break;
         if (d_.stepMode) {
-            upload_dev();
-            launch_step(d_, t, 1, p_.agent, expandVariant_, stream_, timing(K_STEP));
-            flushed_ = false;
+            stage_step(t);
+            if (d_.sharded) stage_exchange(t);
             stage_fold(t);
             continue;
         }
         stage_expand(t);
         if (d_.sharded) {
             stage_pack(t);
-            stage_exchange();
+            stage_exchange(t);
         }
         stage_finish(t);
         stage_fold(t);
@@ -465,14 +482,30 @@ void KgmtPlanner::stage_pack(int t) {
     launch_pack(d_, t, expandBlocks_, stream_, timing(K_PACK));
 }
 
-void KgmtPlanner::stage_exchange() {
+void KgmtPlanner::stage_step(int t) {
+    upload_dev();
+    launch_step(d_, t, 1, p_.agent, expandVariant_, stream_, timing(K_STEP));
+    flushed_ = false;
+}
+
+void KgmtPlanner::stage_exchange(int t) {
     if (!ex_) return;
+    const unsigned long long* send = exchange_send(t);
     if (oneshot_) {
         ++xSeq_;
-        launch_oneshot(inbox_, xSend_, xRecv_, (long long)xWords_, d_.nranks, d_.rank, xSeq_, &d_.status->error,
+        launch_oneshot(inbox_, send, xRecv_, (long long)xWords_, d_.nranks, d_.rank, xSeq_, &d_.status->error,
                        stream_, timing(K_XCHG));
     } else {
-        ex_->allreduce_u64(xSend_, xRecv_, xWords_, stream_);
+        ex_->allreduce_u64(send, xRecv_, xWords_, stream_);
+    }
+}
+
+// k_step mode: complete the last enqueued iteration (insert it, plan t_next) before a read-back
+void KgmtPlanner::flush() {
+    if (d_.stepMode && begun_ && !flushed_) {
+        upload_dev();
+        launch_step(d_, t_next_, 0, p_.agent, expandVariant_, stream_, KernelTiming());
+        flushed_ = true;
     }
 }
 
@@ -505,11 +538,7 @@ void KgmtPlanner::upload_dev() {
 }
 
 void KgmtPlanner::sync() {
-    if (d_.stepMode && begun_ && !flushed_) {   // complete the last iteration (insert, plan t_next)
-        upload_dev();
-        launch_step(d_, t_next_, 0, p_.agent, expandVariant_, stream_, KernelTiming());
-        flushed_ = true;
-    }
+    flush();
     SBMP_HIP(hipStreamSynchronize(stream_));
     wallMs_ = now_ms() - t0_;
     if (d_.timeline && !timelineDumped_ && t_next_ > d_.timelineIter) {
@@ -548,11 +577,7 @@ int KgmtPlanner::last_executed(const std::vector<IterCtrl>& c) const {
 
 bool KgmtPlanner::active() {
     if (!begun_) return false;
-    if (d_.stepMode && !flushed_) {   // the flush pass writes ctrl[t_next] and the goal of t_next - 1
-        upload_dev();
-        launch_step(d_, t_next_, 0, p_.agent, expandVariant_, stream_, KernelTiming());
-        flushed_ = true;
-    }
+    flush();   // k_step mode: the flush pass writes ctrl[t_next] and the goal of t_next - 1
     // ctrl has numIterations + 2 entries, so t_next <= numIterations + 1 is in range
     SBMP_HIP(hipMemcpyAsync(&poll_->ctrl, d_.ctrl + t_next_, sizeof(IterCtrl), hipMemcpyDeviceToHost, stream_));
     SBMP_HIP(hipMemcpyAsync(&poll_->status, d_.status, sizeof(PlannerStatus), hipMemcpyDeviceToHost, stream_));

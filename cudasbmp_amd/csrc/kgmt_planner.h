@@ -139,10 +139,14 @@ public:
     int take_iteration();                 // next iteration number, 0 past numIterations
     void stage_expand(int t);
     void stage_pack(int t);               // sharded ranks only
-    void stage_exchange();                // sharded ranks with an Exchange: the all-reduce
+    void stage_exchange(int t);           // sharded ranks with an Exchange: the all-reduce of t
     void stage_finish(int t);
     void stage_fold(int t);               // every kFoldEvery iterations
-    unsigned long long* exchange_send() const { return xSend_; }
+    void stage_step(int t);               // k_step mode: the iteration's one launch
+    void flush();                         // k_step mode: insert the last iteration, plan the next
+    bool step_mode() const { return d_.stepMode != 0; }
+    // what iteration t sends (sharded k_step alternates two buffers by parity)
+    unsigned long long* exchange_send(int t = 0) const { return (t & 1) ? xSendOdd_ : xSend_; }
     unsigned long long* exchange_recv() const { return xRecv_; }
     size_t exchange_words() const { return xWords_; }
     float4* record_buffer() const { return d_.recOut; }
@@ -186,6 +190,8 @@ private:
     unsigned long long* local_ = nullptr;   // sharded: the owner's block counts + GNew words
     size_t localWords_ = 0;
     unsigned long long* xSend_ = nullptr;
+    unsigned long long* xSendOdd_ = nullptr;   // sharded k_step: the send buffer of odd iterations
+    bool shStep_ = false;                      // sharded rank in k_step mode
     unsigned long long* xRecv_ = nullptr;
     size_t xWords_ = 0;
     bool oneshot_ = false;                   // sharded: the exchange is k_oneshot over IPC-mapped inboxes
@@ -224,11 +230,17 @@ public:
 
     void begin(const float* initial, const float* goal, const float* d_obstacles, int nObs, uint64_t seed) override;
     void enqueue(int iterations) override;
-    void sync() override { r0().sync(); }
+    void sync() override {
+        for (KgmtPlanner* k : ranks_) k->flush();   // every rank's flush pass (GNew words live with their owner)
+        r0().sync();
+    }
     void fold_pending() override {
         for (KgmtPlanner* k : ranks_) k->fold_pending();
     }
-    bool active() override { return r0().active(); }
+    bool active() override {
+        for (KgmtPlanner* k : ranks_) k->flush();
+        return r0().active();
+    }
     void result(sbmp_plan_result* r) override { r0().result(r); }
 
     hipStream_t stream() const override { return stream_; }

@@ -223,6 +223,13 @@ void LocalShardGroup::enqueue(int iterations) {
         int t = 0;
         for (KgmtPlanner* k : ranks_) t = k->take_iteration();   // all ranks advance together
         if (t == 0) break;
+        if (r0().step_mode()) {   // one k_step per rank, then the exchange of t
+            for (KgmtPlanner* k : ranks_) k->stage_step(t);
+            for (int q = 0; q < P; ++q) send[q] = ranks_[q]->exchange_send(t);
+            launch_xsum(send, recv, P, (long long)ranks_[0]->exchange_words(), stream_);
+            for (KgmtPlanner* k : ranks_) k->stage_fold(t);
+            continue;
+        }
         for (KgmtPlanner* k : ranks_) k->stage_expand(t);
         for (KgmtPlanner* k : ranks_) k->stage_pack(t);
         launch_xsum(send, recv, P, (long long)ranks_[0]->exchange_words(), stream_);
