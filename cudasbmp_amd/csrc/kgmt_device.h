@@ -86,8 +86,7 @@ constexpr uint16_t kNoKey = 0xffff;  // child outside the R2 grid (D3)
 // 18.7 -> 14.6 us at 8 replicas).
 constexpr int kDeltaReps = 8;
 constexpr int kNewReps = 8;     // k_step R2New replicas (merged by the next planner)
-constexpr int kMaxStepBlocks = 1024;
-constexpr int kMaxShardStepBlocks = 8192;   // sharded k_step: all ranks' blocks in LDS (8 x 262,144 slots)   // k_step: one int4 of block counts per thread (<= 262,144 slots)
+constexpr int kMaxStepBlocks = 1024;   // k_step: one int4 of block (or row) counts per thread (<= 262,144 slots per rank)
 constexpr int kNoGoalIdx = 0x7fffffff;
 constexpr int kFastDivMax = 1 << 24;   // slot counts up to this use the float-estimate division
 constexpr int kStepEntry = 3;       // k_step list entry: state, (a, steer, dur, parent), (cost, -, -, -)
@@ -186,14 +185,17 @@ struct KgmtDev {
     long long* timelineFin;   // k_finish(timelineIter): [1 + nBlocks][kTimelineStamps], wave 0 of each workgroup
     int timelineIter;
     int obsNaN;   // a register-held obstacle has a NaN coordinate: wave_cull keeps every box
-    // Sharded k_step: per-iteration exchange [R1 delta replicas | packed
-    // block count words (nBlocks, owner-written) | R2New bytes]; this rank's part of
-    // iteration t goes to stepXs[t & 1], stepXr holds the sum over ranks of t - 1.
-    // The flagged children's lists are the record buffers (recOut / recPeer), one
-    // 256-entry list per owned block, read by every rank with system-scope loads.
+    // Sharded k_step: per-iteration exchange [R1 delta replicas | row
+    // words | block words | R2New bytes].  Row b is block b of every rank (global
+    // blocks b P .. b P + P - 1); every rank adds its block's count | goal flag << 16
+    // into row word b, so the sum is the row's; block words are owner-written (count |
+    // (1 + in-block goal index) << 16).  This rank's part of iteration t goes to
+    // stepXs[t & 1], stepXr holds the sum over ranks of t - 1.  The flagged children's
+    // lists are the record buffers (recOut / recPeer), one 256-entry list per owned
+    // block, read by every rank with system-scope loads.
     unsigned long long* stepXs[2];
     const unsigned long long* stepXr;
-    int xCntOff, xNewOff;   // u64 offsets of the count words and of the R2New bytes
+    int xRowOff, xCntOff, xNewOff;   // u64 offsets of the row words, block words and R2New bytes
     // k_step reads this struct from device memory (a copy the host refreshes before a
     // launch when it changed): as a 600-B kernel argument its fields were loaded at
     // entry, spilled to VGPR lanes and reloaded, four serial scalar round trips

@@ -924,38 +924,23 @@ __device__ __forceinline__ void step_scan(const KgmtDev& d, int4 pk, int* sPfx, 
     *jGoal = __builtin_amdgcn_readfirstlane(min(min(sRed[1][0], sRed[1][1]), min(sRed[1][2], sRed[1][3])));
 }
 
-// step_scan for a sharded rank: t-1's packed count words of every rank's blocks
-// (the exchange's count field, up to kMaxShardStepBlocks), `per` consecutive blocks
-// per thread.  Pass 1 keeps each thread's local prefix in LDS, pass 2 adds the
-// thread's base; the lowest goal child is found as in step_scan.
-__device__ __forceinline__ void step_scan_sh(const KgmtDev& d, const SBMP_GAS int* cnt, int* sPfx,
-                                             int (*sRed)[kBlock / kWave], int* A, int* jGoal) {
-    constexpr int kV = kMaxShardStepBlocks / (4 * kBlock);   // int4 loads per thread at most
+// Sharded k_step: the scan runs over rows (block b of every rank), so its size is the
+// rank's block count however many ranks there are.  sPfx[r] = children of the rows
+// before r, *A the total, *gRow the lowest row holding a goal child (kNoGoalIdx if none).
+__device__ __forceinline__ void step_scan_rows(const KgmtDev& d, int4 pk, int* sPfx, int (*sRed)[kBlock / kWave],
+                                               int* A, int* gRow) {
     const int tid = threadIdx.x;
     const int lane = tid & (kWave - 1);
     const int wave = tid >> 6;
-    const int nb4 = (d.nBlocks + 3) & ~3;
-    const int per = ((nb4 + 4 * kBlock - 1) / (4 * kBlock)) * 4;   // multiple of 4, <= 4 kV
-    const int g0 = tid * per;
-    int4 v[kV];
+    const int nRows = d.nBlocks / d.nranks;
+    int loc[4];
+    int run = 0, grow = kNoGoalIdx;
+    const int v4[4] = {pk.x, pk.y, pk.z, pk.w};
 #pragma unroll
-    for (int i = 0; i < kV; ++i)   // every load in flight before the first use
-        if (4 * i < per) v[i] = *reinterpret_cast<const SBMP_GAS int4*>(cnt + min(g0 + 4 * i, nb4 - 4));
-    int run = 0, gloc = kNoGoalIdx;
-#pragma unroll
-    for (int i = 0; i < kV; ++i) {
-        if (4 * i < per) {
-            const int e[4] = {v[i].x, v[i].y, v[i].z, v[i].w};
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const int g = g0 + 4 * i + k;
-                int c, gl;
-                step_unpack(g < nb4 ? e[k] : 0, &c, &gl);
-                if (g <= d.nBlocks) sPfx[g] = run;
-                if (gl >= 0 && gloc == kNoGoalIdx) gloc = run + gl;   // prefixes grow with g
-                run += c;
-            }
-        }
+    for (int e = 0; e < 4; ++e) {
+        loc[e] = run;
+        run += v4[e] & 0xffff;
+        if ((v4[e] >> 16) != 0 && grow == kNoGoalIdx) grow = tid * 4 + e;
     }
     const int incl = wave_incl_sum(run);
     if (lane == kWave - 1) sRed[0][wave] = incl;
@@ -963,13 +948,50 @@ __device__ __forceinline__ void step_scan_sh(const KgmtDev& d, const SBMP_GAS in
     int base = incl - run;
     base += (wave > 0 ? sRed[0][0] : 0) + (wave > 1 ? sRed[0][1] : 0) + (wave > 2 ? sRed[0][2] : 0);
     *A = __builtin_amdgcn_readfirstlane(sRed[0][0] + sRed[0][1] + sRed[0][2] + sRed[0][3]);
-    for (int g = g0; g < g0 + per && g <= d.nBlocks; ++g) sPfx[g] += base;
-    if (tid == 0 && g0 + per * kBlock <= d.nBlocks) sPfx[d.nBlocks] = *A;   // past every thread's range
-    int gmin = (gloc != kNoGoalIdx) ? base + gloc : kNoGoalIdx;
-    gmin = first_lane_value(gmin != kNoGoalIdx, gmin, kNoGoalIdx);
-    if (lane == 0) sRed[1][wave] = gmin;
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+        if (tid * 4 + e <= nRows) sPfx[tid * 4 + e] = base + loc[e];
+    if (tid == kBlock - 1 && nRows == kMaxStepBlocks) sPfx[kMaxStepBlocks] = *A;
+    grow = first_lane_value(grow != kNoGoalIdx, grow, kNoGoalIdx);
+    if (lane == 0) sRed[1][wave] = grow;
     __syncthreads();
-    *jGoal = __builtin_amdgcn_readfirstlane(min(min(sRed[1][0], sRed[1][1]), min(sRed[1][2], sRed[1][3])));
+    *gRow = __builtin_amdgcn_readfirstlane(min(min(sRed[1][0], sRed[1][1]), min(sRed[1][2], sRed[1][3])));
+}
+
+// The P block words of row r (counts | (1 + goal index) << 16), in block order.
+__device__ __forceinline__ void row_words(const KgmtDev& d, int r, int* w) {
+    const SBMP_GAS int* blk = reinterpret_cast<const SBMP_GAS int*>(G(d.stepXr) + d.xCntOff) + (size_t)r * d.nranks;
+#pragma unroll
+    for (int q = 0; q < kMaxRanks; ++q) w[q] = (q < d.nranks) ? blk[q] : 0;
+}
+
+// Position off inside row r -> (global block, index in it), from the row's words.
+__device__ __forceinline__ void row_locate(const KgmtDev& d, const int* w, int r, int off, int* block, int* idx) {
+    int q = 0;
+#pragma unroll
+    for (int k = 0; k < kMaxRanks - 1; ++k) {
+        const int c = w[k] & 0xffff;
+        if (k == q && k + 1 < d.nranks && off >= c) {
+            off -= c;
+            q = k + 1;
+        }
+    }
+    *block = r * d.nranks + q;
+    *idx = off;
+}
+
+// jGoal of a sharded scan: the lowest global index of a goal child, in row gRow.
+__device__ __forceinline__ int row_goal(const KgmtDev& d, const int* sPfx, int gRow) {
+    if (gRow == kNoGoalIdx) return kNoGoalIdx;
+    int w[kMaxRanks];
+    row_words(d, gRow, w);
+    int pre = sPfx[gRow], j = kNoGoalIdx;
+#pragma unroll
+    for (int q = 0; q < kMaxRanks; ++q) {
+        if (q < d.nranks && j == kNoGoalIdx && (w[q] >> 16) != 0) j = pre + (w[q] >> 16) - 1;
+        pre += w[q] & 0xffff;
+    }
+    return __builtin_amdgcn_readfirstlane(j);
 }
 
 // The list entry (state, ctrl, cost) of row j of t-1's flagged children, given the
@@ -1040,8 +1062,9 @@ __device__ __forceinline__ void step_planner(const KgmtDev& d, int t, int expand
     const bool tl = d.timelineFin && t == d.timelineIter && tid == 0;   // diagnostics: entry, publish
     if (tl) G(d.timelineFin)[0] = (long long)__builtin_amdgcn_s_memrealtime();
     // every input at entry
-    int4 pk = make_int4(0, 0, 0, 0);
-    if constexpr (!SH) pk = *reinterpret_cast<const SBMP_GAS int4*>(G(d.stepCnt) + (size_t)pp * kMaxStepBlocks + tid * 4);
+    // t-1's packed counts: blocks, or (sharded) rows of the exchange
+    const int4 pk = SH ? reinterpret_cast<const SBMP_GAS int4*>(G(d.stepXr) + d.xRowOff)[tid]
+                       : *reinterpret_cast<const SBMP_GAS int4*>(G(d.stepCnt) + (size_t)pp * kMaxStepBlocks + tid * 4);
     const IterCtrl pc = G(d.ctrl)[t - 1];
     const int goalIdx = G(d.status)->goalIdx;
     const SBMP_GAS int* tabPrev = G(d.R1) + (size_t)pp * 5 * d.nR1;
@@ -1093,8 +1116,13 @@ __device__ __forceinline__ void step_planner(const KgmtDev& d, int t, int expand
     }
     for (int i = tid; i < d.nR1; i += kBlock) sCovInc[i] = 0;
     int A, jGoal;
-    if constexpr (SH) step_scan_sh(d, reinterpret_cast<const SBMP_GAS int*>(G(d.stepXr) + d.xCntOff), sPfx, sRed, &A, &jGoal);
-    else step_scan(d, pk, sPfx, sRed, &A, &jGoal);
+    if constexpr (SH) {
+        int gRow;
+        step_scan_rows(d, pk, sPfx, sRed, &A, &gRow);
+        jGoal = row_goal(d, sPfx, gRow);
+    } else {
+        step_scan(d, pk, sPfx, sRed, &A, &jGoal);
+    }
     const StepPlan q = step_plan(d, t, expand, pc, goalIdx, A, jGoal);
     SBMP_GAS int* tabCur = G(d.R1) + (size_t)cp * 5 * d.nR1;
     if (!q.ranPrev) {   // t-1 did not run: the loop has ended; carry the tables forward
@@ -1219,12 +1247,20 @@ __device__ __forceinline__ void step_planner(const KgmtDev& d, int t, int expand
     // workgroup is idle.
     if (t > 1 && A <= kPlannerInsertMax) {
         const int n = min(q.nIns, d.M - q.tsPrev);   // D13: the reference writes past M
-        // list entry of row j: block lo with sPfx[lo] <= j < sPfx[lo + 1]
+        // list entry of row j: block (sharded: row) lo with sPfx[lo] <= j < sPfx[lo + 1]
+        const int nS = SH ? d.nBlocks / d.nranks : d.nBlocks;
         auto entry = [&](int j) {
             int lo = 0;
-            for (int step = (SH ? kMaxShardStepBlocks : kMaxStepBlocks) / 2; step > 0; step >>= 1)
-                if (lo + step < d.nBlocks && sPfx[lo + step] <= j) lo += step;
-            return list_entry<SH>(d, pp, lo, j - sPfx[lo]);
+            for (int step = kMaxStepBlocks / 2; step > 0; step >>= 1)
+                if (lo + step < nS && sPfx[lo + step] <= j) lo += step;
+            if constexpr (SH) {
+                int w[kMaxRanks], blk, idx;
+                row_words(d, lo, w);
+                row_locate(d, w, lo, j - sPfx[lo], &blk, &idx);
+                return list_entry<SH>(d, pp, blk, idx);
+            } else {
+                return list_entry<SH>(d, pp, lo, j - sPfx[lo]);
+            }
         };
         auto put = [&](int j, float4 s4, float4 u4, float c) {
             const int dst = q.tsPrev + j;
@@ -1275,7 +1311,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) voi
     constexpr bool kLdsObs = (OBS == kObsLds || OBS == kObsLds4);
     constexpr int kRegObs = obs_in_registers(OBS);
     int* const sPfx = reinterpret_cast<int*>(sDyn + (kLdsObs ? d.nObs : 0));
-    uint32_t* const sNew = reinterpret_cast<uint32_t*>(sPfx + d.nBlocks + 1);
+    uint32_t* const sNew = reinterpret_cast<uint32_t*>(sPfx + (SH ? d.nBlocks / d.nranks : d.nBlocks) + 1);
     if (blockIdx.x == 0) {
         step_planner<SH>(d, t, expand, sPfx, sRed, sCovInc, sPart);
         return;
@@ -1315,9 +1351,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) voi
 
     // ---- loads that depend on nothing else (the control block as a plain load: a
     // waiting scalar load would serialise behind the scan)
-    int4 pk = make_int4(0, 0, 0, 0);
-    if constexpr (!SH) pk = *reinterpret_cast<const SBMP_GAS int4*>(cntP + (size_t)pp * kMaxStepBlocks + tid * 4);
+    const int4 pk = SH ? reinterpret_cast<const SBMP_GAS int4*>(G(d.stepXr) + d.xRowOff)[tid]
+                       : *reinterpret_cast<const SBMP_GAS int4*>(cntP + (size_t)pp * kMaxStepBlocks + tid * 4);
     const IterCtrl pc = ctrlP[t - 1];
+    int rowW[SH ? kMaxRanks : 1];   // sharded: the block words of this workgroup's row (its inserts)
+    if constexpr (SH) row_words(d, b, rowW);
     const int goalIdx = statusP->goalIdx;
     const uint4 ra = rngAP[slot];
     const uint2 rb = rngBP[slot];
@@ -1332,8 +1370,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) voi
     ChildCtl ctl = draw_controls<AGENT>(rs, d);
     asm volatile("" : "+v"(ctl.a), "+v"(ctl.steer), "+v"(ctl.dur), "+v"(ctl.dt), "+v"(ctl.tanS));
     int A, jGoal;
-    if constexpr (SH) step_scan_sh(d, reinterpret_cast<const SBMP_GAS int*>(G(d.stepXr) + d.xCntOff), sPfx, sRed, &A, &jGoal);
-    else step_scan(d, pk, sPfx, sRed, &A, &jGoal);
+    if constexpr (SH) {
+        int gRow;
+        step_scan_rows(d, pk, sPfx, sRed, &A, &gRow);
+        jGoal = row_goal(d, sPfx, gRow);
+    } else {
+        step_scan(d, pk, sPfx, sRed, &A, &jGoal);
+    }
     SBMP_STAMP(1);
     // the control block and the goal index were loaded per lane (vector loads do not
     // wait behind the scan's scalar work); the plan is wave-uniform, so scalar code
@@ -1359,9 +1402,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) voi
     // index).  Each entry carries its cost, so this is one load and three stores; an
     // expanding block issues it right behind its parent loads (one round trip).
     const bool selfInsert = A > kPlannerInsertMax;   // else the planner workgroup inserts
-    auto insert_block = [&](int lo) {   // t-1's flagged children of global block lo
-        if (tid < sPfx[lo + 1] - sPfx[lo]) {
-            const int j = sPfx[lo] + tid;
+    auto insert_block = [&](int lo, int j0, int cnt) {   // t-1's flagged children of global block lo: rows j0 ..
+        if (tid < cnt) {
+            const int j = j0 + tid;
             const int dst = q.tsPrev + j;
             if (j < q.nIns && dst < d.M) {   // D13: the reference writes past M here
                 const SBMP_GAS float4* e = list_entry<SH>(d, pp, lo, tid);
@@ -1376,10 +1419,15 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) voi
     };
     auto insert_prev = [&]() {
         if (t > 1 && selfInsert) {
-            if constexpr (SH) {   // every rank holds the whole tree: blocks b P .. b P + P - 1
-                for (int r = 0; r < d.nranks; ++r) insert_block(b * d.nranks + r);
+            if constexpr (SH) {   // every rank holds the whole tree: row b = blocks b P .. b P + P - 1
+                int j0 = sPfx[b];
+                for (int r = 0; r < d.nranks; ++r) {
+                    const int c = rowW[r] & 0xffff;
+                    insert_block(b * d.nranks + r, j0, c);
+                    j0 += c;
+                }
             } else {
-                insert_block(b);
+                insert_block(b, sPfx[b], sPfx[b + 1] - sPfx[b]);
             }
         }
     };
@@ -1407,17 +1455,18 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) voi
         const int jA = __builtin_amdgcn_readlane(j, (int)__builtin_ctzll(need));
         const int jB = __builtin_amdgcn_readlane(j, 63 - (int)__builtin_clzll(need));
         int lo = 0;
-        if (jB - jA <= 1 && d.nBlocks <= kMaxStepBlocks) {   // two 32-ary levels cover 1,024 blocks
+        const int nS = SH ? d.nBlocks / d.nranks : d.nBlocks;   // scan entries: blocks, or (sharded) rows
+        if (jB - jA <= 1) {
             const int jj = (lane < 32) ? jA : jB;
             const int sub = lane & 31;
             int idx = sub * 32;
-            unsigned long long m = __ballot((idx < d.nBlocks ? sPfx[idx] : INT_MAX) <= jj);
+            unsigned long long m = __ballot((idx < nS ? sPfx[idx] : INT_MAX) <= jj);
             const int cA = __popcll(m & 0xffffffffull) - 1, cB = __popcll(m >> 32) - 1;
             idx = ((lane < 32) ? cA : cB) * 32 + sub;
-            m = __ballot((idx < d.nBlocks ? sPfx[idx] : INT_MAX) <= jj);
+            m = __ballot((idx < nS ? sPfx[idx] : INT_MAX) <= jj);
             lo = (j == jA) ? cA * 32 + __popcll(m & 0xffffffffull) - 1 : cB * 32 + __popcll(m >> 32) - 1;
         } else {
-            int hi = d.nBlocks;
+            int hi = nS;
             while (hi - lo > 1) {
                 const int mid = (lo + hi) >> 1;
                 if (sPfx[mid] <= j) lo = mid;
@@ -1425,7 +1474,14 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) voi
             }
         }
         if (fromList) {
-            src = list_entry<SH>(d, pp, lo, j - sPfx[lo]);
+            if constexpr (SH) {   // the row's blocks: one more (L2) round trip for their words
+                int w[kMaxRanks], blk, idx;
+                row_words(d, lo, w);
+                row_locate(d, w, lo, j - sPfx[lo], &blk, &idx);
+                src = list_entry<SH>(d, pp, blk, idx);
+            } else {
+                src = list_entry<SH>(d, pp, lo, j - sPfx[lo]);
+            }
             srcCost = reinterpret_cast<const SBMP_GAS float*>(src + 2);
         }
     }
@@ -1609,7 +1665,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) voi
         if (g1 != kNoGoalIdx) gmin = c0 + g1;
         if (g0 != kNoGoalIdx) gmin = g0;
         const int cw = (c0 + c1 + c2 + c3) | ((gmin == kNoGoalIdx ? 0 : gmin + 1) << 16);
-        if constexpr (SH) reinterpret_cast<SBMP_GAS int*>(G(d.stepXs[cp]) + d.xCntOff)[gb] = cw;
+        if constexpr (SH) {   // the block word, and this rank's part of row b (the exchange sums the row)
+            reinterpret_cast<SBMP_GAS int*>(G(d.stepXs[cp]) + d.xCntOff)[gb] = cw;
+            reinterpret_cast<SBMP_GAS int*>(G(d.stepXs[cp]) + d.xRowOff)[b] =
+                (c0 + c1 + c2 + c3) | ((gmin == kNoGoalIdx ? 0 : 1) << 16);
+        }
         else G(d.stepCnt)[(size_t)cp * kMaxStepBlocks + b] = cw;
     }
     SBMP_STAMP(6);
@@ -1799,7 +1859,8 @@ template <int AGENT, bool SH>
 static void launch_step_form(const KgmtDev& d, int t, int expand, int variant, hipStream_t s,
                              const KernelTiming& tm) {
     // dynamic LDS: [LDS obstacles][block prefix: nBlocks + 1 ints][R2New bits: nR2 / 32 words]
-    const size_t pfx = sizeof(int) * ((size_t)d.nBlocks + 1) + sizeof(uint32_t) * (size_t)(d.nR2 / 32);
+    const size_t nS = SH ? d.nBlocks / d.nranks : d.nBlocks;   // scan entries: blocks, or rows
+    const size_t pfx = sizeof(int) * (nS + 1) + sizeof(uint32_t) * (size_t)(d.nR2 / 32);
     const size_t shm = sizeof(float4) * (size_t)d.nObs + pfx;   // LDS obstacle forms
     const int blocks = SH ? d.nBlocks / d.nranks : d.nBlocks;
     const dim3 grid(1 + blocks), block(kBlock);   // workgroup 0 plans, 1.. expand

@@ -186,17 +186,19 @@ KgmtPlanner::KgmtPlanner(const sbmp_kgmt_params& p, int nranks, int rank, Exchan
         // Sharded: [R1 delta replicas | block prefixes pfx | rank totals | R2New bytes]
         //          is all-reduced; block counts and GNew words are the owner's alone
         //          (a separate local buffer), since the inserts are record-driven.
-        // Sharded k_step (one launch per iteration): [R1 delta replicas | packed block
-        //          count words (nBlocks, int4-readable) | R2New bytes], two send parities.
+        // Sharded k_step (one launch per iteration): [R1 delta replicas | row words
+        //          (kMaxStepBlocks, summed over ranks) | block words (nBlocks, owner-
+        //          written) | R2New bytes], two send parities.
         const bool sharded = nranks > 1 || ex;
         const char* sv = std::getenv("SBMP_STEP");
-        shStep_ = sharded && d.nBlocks <= kMaxShardStepBlocks && !(sv && atoi(sv) == 0);
+        shStep_ = sharded && d.nBlocks / nranks <= kMaxStepBlocks && !(sv && atoi(sv) == 0);
+        const size_t rowWords = shStep_ ? kMaxStepBlocks / 2 : 0;
         const size_t dWords = round_up((long long)kDeltaReps * d.nR1, 2);
         const size_t bcWords = round_up(d.nBlocks, 4) / 2, r2Words = round_up(d.nR2, 16) / 8;
         const size_t pfxWords = round_up(d.nBlocks + 1, 4) / 2, totWords = kMaxRanks / 2;
         unsigned long long* local = nullptr;
         if (shStep_) {
-            xWords_ = dWords + bcWords + r2Words;
+            xWords_ = dWords + rowWords + bcWords + r2Words;
             local = alloc<unsigned long long>(bcWords + (size_t)nWords);
             localWords_ = bcWords + (size_t)nWords;
             local_ = local;
@@ -214,8 +216,9 @@ KgmtPlanner::KgmtPlanner(const sbmp_kgmt_params& p, int nranks, int rank, Exchan
         d.stepXs[0] = shStep_ ? xSend_ : nullptr;
         d.stepXs[1] = shStep_ ? xSendOdd_ : nullptr;
         d.stepXr = shStep_ ? xRecv_ : nullptr;
-        d.xCntOff = (int)dWords;
-        d.xNewOff = (int)(dWords + bcWords);
+        d.xRowOff = (int)dWords;
+        d.xCntOff = (int)(dWords + rowWords);
+        d.xNewOff = (int)(dWords + rowWords + bcWords);
         int* bc = reinterpret_cast<int*>(sharded ? local : xSend_ + dWords);
         unsigned long long* gn = sharded ? local + bcWords : xSend_ + dWords + bcWords;
         d.blockCountOut = bc;
