@@ -882,8 +882,11 @@ __device__ __forceinline__ void step_unpack(int v, int* cnt, int* goal) {
 }
 
 // Scan of iteration t-1's packed block counts (4 per thread, kMaxStepBlocks = 4 x
-// kBlock): sPfx[g] = flagged children of the blocks before g (g <= nBlocks), *A the
-// total, *jGoal the lowest global index of a flagged child in the goal region.
+// kBlock) with one barrier: sPfx[g] = flagged children of the blocks before g (g <=
+// nBlocks), *A the total, *jGoal the lowest global index of a flagged child in the
+// goal region.  Each wave publishes its total and its lowest goal index relative to
+// its own start before the barrier, so A and jGoal are known right after it; sPfx is
+// written after it and needs the caller's next barrier before other waves read it.
 __device__ __forceinline__ void step_scan(const KgmtDev& d, int4 pk, int* sPfx, int (*sRed)[kBlock / kWave], int* A,
                                           int* jGoal) {
     const int tid = threadIdx.x;
@@ -901,27 +904,32 @@ __device__ __forceinline__ void step_scan(const KgmtDev& d, int4 pk, int* sPfx, 
         run += c;
     }
     const int incl = wave_incl_sum(run);
-    if (lane == kWave - 1) sRed[0][wave] = incl;
-    __syncthreads();
-    int base = incl - run;
-    base += (wave > 0 ? sRed[0][0] : 0) + (wave > 1 ? sRed[0][1] : 0) + (wave > 2 ? sRed[0][2] : 0);
-    // uniform by construction; readfirstlane so the plan that follows is scalar code
-    *A = __builtin_amdgcn_readfirstlane(sRed[0][0] + sRed[0][1] + sRed[0][2] + sRed[0][3]);
+    const int excl = incl - run;   // this thread's start within its wave
     // Prefixes grow with g and a goal child's in-block index is below its block's
     // count, so the lowest g holding a goal child has the lowest global index.
-    int gmin = kNoGoalIdx;
+    int gl = kNoGoalIdx;
 #pragma unroll
-    for (int e = 3; e >= 0; --e) {
-        const int g = tid * 4 + e;
-        const int pf = base + loc[e];
-        if (g <= d.nBlocks) sPfx[g] = pf;
-        if (gl4[e] >= 0) gmin = pf + gl4[e];
-    }
-    if (tid == kBlock - 1 && d.nBlocks == kMaxStepBlocks) sPfx[kMaxStepBlocks] = *A;
-    gmin = first_lane_value(gmin != kNoGoalIdx, gmin, kNoGoalIdx);
-    if (lane == 0) sRed[1][wave] = gmin;
+    for (int e = 3; e >= 0; --e)
+        if (gl4[e] >= 0) gl = excl + loc[e] + gl4[e];
+    gl = first_lane_value(gl != kNoGoalIdx, gl, kNoGoalIdx);
+    if (lane == kWave - 1) sRed[0][wave] = incl;
+    if (lane == 0) sRed[1][wave] = gl;
     __syncthreads();
-    *jGoal = __builtin_amdgcn_readfirstlane(min(min(sRed[1][0], sRed[1][1]), min(sRed[1][2], sRed[1][3])));
+    const int w0 = sRed[0][0], w1 = sRed[0][1], w2 = sRed[0][2], w3 = sRed[0][3];
+    // uniform by construction; readfirstlane so the plan that follows is scalar code
+    *A = __builtin_amdgcn_readfirstlane(w0 + w1 + w2 + w3);
+    const int g0 = sRed[1][0], g1 = sRed[1][1], g2 = sRed[1][2], g3 = sRed[1][3];
+    int jg = kNoGoalIdx;   // the lowest wave holding one has the lowest index
+    if (g3 != kNoGoalIdx) jg = w0 + w1 + w2 + g3;
+    if (g2 != kNoGoalIdx) jg = w0 + w1 + g2;
+    if (g1 != kNoGoalIdx) jg = w0 + g1;
+    if (g0 != kNoGoalIdx) jg = g0;
+    *jGoal = __builtin_amdgcn_readfirstlane(jg);
+    const int base = excl + (wave > 0 ? w0 : 0) + (wave > 1 ? w1 : 0) + (wave > 2 ? w2 : 0);
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+        if (tid * 4 + e <= d.nBlocks) sPfx[tid * 4 + e] = base + loc[e];
+    if (tid == kBlock - 1 && d.nBlocks == kMaxStepBlocks) sPfx[kMaxStepBlocks] = *A;
 }
 
 // Sharded k_step: the scan runs over rows (block b of every rank), so its size is the
@@ -1018,6 +1026,25 @@ struct StepPlan {
     int tsPrev, treeSize, gLo, H, grid, nIns, newGoal, runT, nG, k, nExp, S;
     bool executes;
 };
+// A plan read back from LDS, made wave-uniform (scalar registers).
+__device__ __forceinline__ StepPlan uniform_plan(const StepPlan& s) {
+    StepPlan q;
+    q.ranPrev = __builtin_amdgcn_readfirstlane((int)s.ranPrev) != 0;
+    q.tsPrev = __builtin_amdgcn_readfirstlane(s.tsPrev);
+    q.treeSize = __builtin_amdgcn_readfirstlane(s.treeSize);
+    q.gLo = __builtin_amdgcn_readfirstlane(s.gLo);
+    q.H = __builtin_amdgcn_readfirstlane(s.H);
+    q.grid = __builtin_amdgcn_readfirstlane(s.grid);
+    q.nIns = __builtin_amdgcn_readfirstlane(s.nIns);
+    q.newGoal = __builtin_amdgcn_readfirstlane(s.newGoal);
+    q.runT = __builtin_amdgcn_readfirstlane(s.runT);
+    q.nG = __builtin_amdgcn_readfirstlane(s.nG);
+    q.k = __builtin_amdgcn_readfirstlane(s.k);
+    q.nExp = __builtin_amdgcn_readfirstlane(s.nExp);
+    q.S = __builtin_amdgcn_readfirstlane(s.S);
+    q.executes = __builtin_amdgcn_readfirstlane((int)s.executes) != 0;
+    return q;
+}
 __device__ __forceinline__ StepPlan step_plan(const KgmtDev& d, int t, int expand, const IterCtrl& pc, int goalIdx,
                                               int A, int jGoal) {
     StepPlan q;
@@ -1302,6 +1329,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) voi
     const KgmtDev& d = *dp;
     extern __shared__ float4 sDyn[];   // [LDS obstacles][prefix: nBlocks + 1 ints][R2New bits: nR2 / 32]
     __shared__ int sR1P[kMaxR1];
+    __shared__ StepPlan sPlan;
     __shared__ int sWaveCnt[kBlock / kWave];
     __shared__ int sWaveGoal[kBlock / kWave];
     __shared__ int sRed[2][kBlock / kWave];
@@ -1370,23 +1398,37 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) voi
     ChildCtl ctl = draw_controls<AGENT>(rs, d);
     asm volatile("" : "+v"(ctl.a), "+v"(ctl.steer), "+v"(ctl.dur), "+v"(ctl.dt), "+v"(ctl.tanS));
     int A, jGoal;
+    // the control block and the goal index were loaded per lane (vector loads do not
+    // wait behind the scan's scalar work); the plan is wave-uniform, so scalar code
+    auto plan = [&]() {
+        IterCtrl pcu = pc;
+        pcu.executed = __builtin_amdgcn_readfirstlane(pc.executed);
+        pcu.treeSize = __builtin_amdgcn_readfirstlane(pc.treeSize);
+        pcu.gLo = __builtin_amdgcn_readfirstlane(pc.gLo);
+        pcu.nExp = __builtin_amdgcn_readfirstlane(pc.nExp);
+        pcu.H = __builtin_amdgcn_readfirstlane(pc.H);
+        return step_plan(d, t, expand, pcu, __builtin_amdgcn_readfirstlane(goalIdx), A, jGoal);
+    };
+    StepPlan q;
     if constexpr (SH) {
         int gRow;
         step_scan_rows(d, pk, sPfx, sRed, &A, &gRow);
         jGoal = row_goal(d, sPfx, gRow);
+        SBMP_STAMP(1);
+        q = plan();
     } else {
+        // One wave per workgroup computes the plan while the others write their prefix
+        // entries; the barrier that publishes sPfx publishes the plan.  (Every wave
+        // computing it kept the CU's one scalar unit busy for 16 waves at once.)
         step_scan(d, pk, sPfx, sRed, &A, &jGoal);
+        SBMP_STAMP(1);
+        if (wave == 0) {
+            const StepPlan q0 = plan();
+            if (lane == 0) sPlan = q0;
+        }
+        __syncthreads();
+        q = uniform_plan(sPlan);
     }
-    SBMP_STAMP(1);
-    // the control block and the goal index were loaded per lane (vector loads do not
-    // wait behind the scan's scalar work); the plan is wave-uniform, so scalar code
-    IterCtrl pcu = pc;
-    pcu.executed = __builtin_amdgcn_readfirstlane(pc.executed);
-    pcu.treeSize = __builtin_amdgcn_readfirstlane(pc.treeSize);
-    pcu.gLo = __builtin_amdgcn_readfirstlane(pc.gLo);
-    pcu.nExp = __builtin_amdgcn_readfirstlane(pc.nExp);
-    pcu.H = __builtin_amdgcn_readfirstlane(pc.H);
-    const StepPlan q = step_plan(d, t, expand, pcu, __builtin_amdgcn_readfirstlane(goalIdx), A, jGoal);
     if (!q.ranPrev) return;
 
     // ---- D6 clear of this block's words of t-1 (KGMT.cu:231,556)

@@ -229,8 +229,9 @@ def test_full_size_properties(fix_clear, d_obs, obstacles, oracle_lib):
     (2, dict(agent="point", samplesPerIteration=2048, maxTreeSize=100000, numIterations=12, goalThreshold=0.0), 5),
 ])
 def test_local_shard_group_bit_exact(P, kw, seed, d_obs, obstacles, oracle_lib):
-    """The sharded data flow (owned slots, k_pack records, summed exchange buffer,
-    every rank inserting every block) with P ranks on one GPU equals the oracle."""
+    """The sharded data flow (owned slots, one k_step per rank and iteration, the
+    owners' lists read through the record buffers, the summed exchange buffer, every
+    rank inserting its row of blocks) with P ranks on one GPU equals the oracle."""
     from cudasbmp_amd import KGMT
     cfg = dict(DEMO)
     extra = {k: kw[k] for k in ("samplesPerIteration", "agent", "fixGNewClear", "batchRule") if k in kw}
@@ -242,10 +243,28 @@ def test_local_shard_group_bit_exact(P, kw, seed, d_obs, obstacles, oracle_lib):
     assert_same_state(g, o, label=f"P={P} {kw}")
 
 
+@pytest.mark.parametrize("P,seed", [(2, 1), (4, 2)])
+def test_local_shard_group_k_step_goal(P, seed, d_obs, obstacles, oracle_lib):
+    """Sharded ranks take k_step (no k_expand / k_pack / k_finish launch), and the goal
+    found through the exchanged row and block words stops the run where the oracle's does."""
+    from cudasbmp_amd import KGMT
+    cfg = dict(DEMO)
+    g = KGMT(**cfg, _local_group=P)
+    g.set_profiling(True)
+    r = g.plan(DEMO_INITIAL, DEMO_GOAL, d_obs, len(obstacles), seed=seed)
+    stats = g.kernel_stats()
+    assert stats["k_step"][0] > 0
+    assert all(stats.get(k, (0, 0.0))[0] == 0 for k in ("k_expand", "k_pack", "k_finish"))
+    assert r.goalIndex >= 0, "demo seeds solve"
+    o = _oracle(cfg, {})
+    o.plan(DEMO_INITIAL, DEMO_GOAL, obstacles, seed)
+    assert_same_state(g, o, label=f"P={P} goal")
+
+
 def test_rccl_single_rank_sharded_path(d_obs, obstacles, oracle_lib):
     """The RCCL rank path end to end on one GPU: ncclCommInitRank, the fused
     ncclAllReduce per iteration, the IPC record-buffer exchange (own buffer) and
-    the R2 counter all-reduce at export, with k_pack / record reads in the loop."""
+    the R2 counter all-reduce at export, with k_step reading the lists through it."""
     import ctypes
     from cudasbmp_amd import KGMT
     from cudasbmp_amd import _native as nat
