@@ -244,6 +244,22 @@ __device__ __forceinline__ void store_wt(uint2* base, int i, uint2 v) {
     __builtin_amdgcn_raw_buffer_store_b64(sbmp_u32x2{v.x, v.y}, wt_rsrc(base), i * 8, 0, kCpolSc1);
 }
 
+// Slot i's XORWOW state for i < n, zeros with no memory access for i >= n: the
+// buffer's num_records is the n slots' bytes, and a raw buffer load whose offset is
+// at or past num_records returns 0 (k_expand: slots in [S, H) of a launch whose batch
+// is below its high-water mark read nothing).  Offsets of the other lanes also get
+// bit 31 set (CK's invalid-element form), past any num_records below 2 GiB.
+__device__ __forceinline__ uint4 load_rng_a(const uint4* base, int i, int n) {
+    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint4*>(base), (short)0, n * 16, kBufferDword3);
+    const sbmp_u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, (i < n ? 0 : (int)0x80000000) + i * 16, 0, 0);
+    return make_uint4(v[0], v[1], v[2], v[3]);
+}
+__device__ __forceinline__ uint2 load_rng_b(const uint2* base, int i, int n) {
+    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint2*>(base), (short)0, n * 8, kBufferDword3);
+    const sbmp_u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(r, (i < n ? 0 : (int)0x80000000) + i * 8, 0, 0);
+    return make_uint2(v[0], v[1]);
+}
+
 // Inclusive prefix sum over the 64 lanes of a wave with DPP: shifts by 1, 2, 4, 8
 // inside each 16-lane row, then the row totals by row_bcast:15 / row_bcast:31.  Every
 // lane must be active.  (__shfl_up compiles to ds_bpermute, one LDS round trip per step.)

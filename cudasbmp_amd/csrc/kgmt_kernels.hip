@@ -171,9 +171,8 @@ __global__ __launch_bounds__(kBlock) void k_expand(KgmtDev d, int t) {
     // Latency: every load that does not depend on the control block is issued
     // before it (slot arrays are allocated to a whole number of workgroups; the
     // score buffer of iteration t is t & 1); the control block is one scalar load;
-    // the parent-row load follows it directly.
-    const uint4 ra = d.rngA[slot];
-    const uint2 rb = d.rngB[slot];
+    // the parent-row load and the active slots' XORWOW states follow it directly
+    // (both are needed only when propagation starts; slots in [S, H) read nothing).
     const unsigned long long oldWord = (lane == 0) ? d.gnewOut[slot >> 6] : 0ull;   // this rank's own words
     const float scoreReg = (tid < d.nR1) ? d.R1Score[(t & 1) * d.nR1 + tid] : 0.0f;
     const float4 obsReg = (kLdsObs && tid < d.nObs) ? d.obstacles[tid] : make_float4(0.f, 0.f, 0.f, 0.f);
@@ -194,6 +193,8 @@ __global__ __launch_bounds__(kBlock) void k_expand(KgmtDev d, int t) {
     const int g = !act ? 0 : slot_div(d, slot, c.k);   // slot = g*k + i
     const int parent = act ? c.gLo + g : 0;
     const float4 p = d.treeState[parent];
+    const uint4 ra = load_rng_a(d.rngA, slot, c.S);   // act == slot < S
+    const uint2 rb = load_rng_b(d.rngB, slot, c.S);
 
     if (tid < d.nR1) sScore[tid] = scoreReg;
     sR1P[tid] = 0;   // nR1 == kBlock
