@@ -1,10 +1,10 @@
 """The cross-process sharded HIP path with two real processes on one GPU.
 
-Each process is one rank of sbmp_kgmt_create_sharded_host: the real k_expand /
-k_pack / k_finish kernels, record buffers written with system-scope stores and
-read by the peer over HIP IPC (hipIpcGetMemHandle / hipIpcOpenMemHandle, handles
-exchanged by an allgather), and the fused exchange buffer all-reduced every
-iteration, either by the default one-shot exchange (each rank stores its buffer into
+Each process is one rank of sbmp_kgmt_create_sharded_host: the real sharded k_step
+kernel (one launch per iteration), each rank's lists of accepted children written to
+its record buffer with system-scope stores and read by the peer over HIP IPC
+(hipIpcGetMemHandle / hipIpcOpenMemHandle, handles exchanged by an allgather), and
+the fused exchange buffer all-reduced every iteration, either by the default one-shot exchange (each rank stores its buffer into
 every rank's IPC-mapped inbox and raises flags; both processes' kernels meet on the
 GPU; the inboxes are uncached device memory) as its own k_oneshot launch, or, with
 SBMP_EXCHANGE=collective, by the Exchange's all-reduce.
@@ -33,8 +33,9 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _rank_main(rank, port, kw, seed, out_dir, exchange):
+def _rank_main(rank, port, kw, seed, out_dir, exchange, delay=0.0):
     import sys
+    import time
     sys.path.insert(0, ROOT)
     if exchange == "collective":
         os.environ["SBMP_EXCHANGE"] = exchange
@@ -52,6 +53,8 @@ def _rank_main(rank, port, kw, seed, out_dir, exchange):
     extra = {k: kw[k] for k in ("samplesPerIteration", "batchRule", "fixGNewClear") if k in kw}
     cfg.update({k: v for k, v in kw.items() if k not in extra})
     g = KGMT(**cfg, **extra, _host_sharded=(TorchCollectives(dist), WORLD, rank))
+    if rank == 1 and delay:
+        time.sleep(delay)   # process skew before the first exchange (begin() holds a host barrier)
     r = g.plan(DEMO_INITIAL, DEMO_GOAL, DeviceBuffer(obs), len(obs), seed=seed)
     s, p, c = g.tree()
     G, GN = g.flags()          # GNew words live with their owner: merged by the all-reduce
@@ -65,19 +68,22 @@ def _rank_main(rank, port, kw, seed, out_dir, exchange):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("kw,seed,exchange", [
-    (dict(), 3, "oneshot"),
+@pytest.mark.parametrize("kw,seed,exchange,delay", [
+    (dict(), 3, "oneshot", 0.0),
     (dict(samplesPerIteration=4096, batchRule="fill", maxTreeSize=200000, numIterations=15, goalThreshold=0.0), 21,
-     "oneshot"),
-    (dict(fixGNewClear=True, numIterations=40), 8, "oneshot"),
-    (dict(), 3, "collective"),
+     "oneshot", 0.0),
+    (dict(fixGNewClear=True, numIterations=40), 8, "oneshot", 0.0),
+    (dict(), 3, "collective", 0.0),
     (dict(samplesPerIteration=4096, batchRule="fill", maxTreeSize=200000, numIterations=15, goalThreshold=0.0), 21,
-     "collective"),
+     "collective", 0.0),
+    # rank 1 starts 3 s late (round 2's exchange gave up after 1 s)
+    (dict(samplesPerIteration=4096, batchRule="fill", maxTreeSize=200000, numIterations=15, goalThreshold=0.0), 21,
+     "oneshot", 3.0),
 ])
-def test_two_processes_one_gpu_bit_exact(kw, seed, exchange, tmp_path, obstacles, oracle_lib):
+def test_two_processes_one_gpu_bit_exact(kw, seed, exchange, delay, tmp_path, obstacles, oracle_lib):
     ctx = mp.get_context("spawn")
     port = _free_port()
-    procs = [ctx.Process(target=_rank_main, args=(r, port, kw, seed, str(tmp_path), exchange))
+    procs = [ctx.Process(target=_rank_main, args=(r, port, kw, seed, str(tmp_path), exchange, delay))
              for r in range(WORLD)]
     for pr in procs:
         pr.start()
