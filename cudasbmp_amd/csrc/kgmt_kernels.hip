@@ -1576,8 +1576,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) voi
     const bool look = act && valid && q2 >= 0;
     unsigned long long sw = 0ull, aw = 0ull;
     if (look) {
-        sw = __hip_atomic_load(pubCur + q1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        aw = __hip_atomic_load(pubCur + d.nR1 + (q2 >> 5), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        // First attempt: plain loads.  The L2 of this XCD holds no line of pubCur from
+        // before this launch (kernel-start acquire), so the first wave of the XCD to
+        // load a line after the planner published brings it in and later waves hit L2
+        // instead of each going to memory; a line loaded before publication carries an
+        // older tag, and the re-read below (agent scope) corrects it.
+        sw = pubCur[q1];
+        aw = pubCur[d.nR1 + (q2 >> 5)];
     }
     float u = 0.0f;
     float4 cs = make_float4(0.f, 0.f, 0.f, 0.f), cc = cs;   // this slot's child (state, ctrl)
