@@ -768,17 +768,24 @@ __device__ __forceinline__ bool car_theta_bounded(float4 p, const ChildCtl& ctl,
 
 // PH: some lane of the wave may pass 105615 (car_theta_bounded failed): sincos_pred's
 // per-step check and Payne-Hanek branch; otherwise Cody-Waite alone.
+// The wave's cull for car_euler_fast, taken once before the caller picks the PH form
+// (inside each form the compiler kept the box flags as lane booleans across the branch).
+template <int OBS>
+__device__ __forceinline__ WaveCull car_cull(float4 p, const ChildCtl& ctl, const KgmtDev& d, const float4* obs) {
+    const float T = ctl.dur;
+    const float r = T * __builtin_fabsf(p.w) + 0.5f * __builtin_fabsf(ctl.a) * T * T;
+    return wave_cull<OBS>(p.x, p.y, r, r, obs, d);
+}
+
 template <int OBS, bool PH>
 __device__ __forceinline__ bool car_euler_fast(float4 p, const ChildCtl& ctl, const KgmtDev& d, const float4* obs,
-                                               ChildOut& out) {
+                                               const WaveCull& cull, ChildOut& out) {
     constexpr int NOBS = obs_in_registers(OBS);
     const float a = ctl.a, T = ctl.dur, dt = ctl.dt;
     // (v, theta): v in the low half, so the packed products broadcast it without a copy
     sbmp_f32x2 xy = {p.x, p.y}, vt = {p.w, p.z};
     const sbmp_f32x2 dt2 = {dt, dt}, wh = {d.width, d.height};
     const float invL = d.invAgentLength;
-    const float r = T * __builtin_fabsf(p.w) + 0.5f * __builtin_fabsf(a) * T * T;
-    const WaveCull cull = wave_cull<OBS>(p.x, p.y, r, r, obs, d);
     unsigned kept = __builtin_amdgcn_readfirstlane(cull.boxes);   // wave-uniform (a ballot)
     float aliveF = 1.0f;   // 1 alive, 0 ended: a float, so no lane mask is carried across steps
     for (int i = 0; i < d.numDisc; ++i) {

@@ -893,43 +893,53 @@ __device__ __forceinline__ void step_scan(const KgmtDev& d, int4 pk, int* sPfx, 
     const int tid = threadIdx.x;
     const int lane = tid & (kWave - 1);
     const int wave = tid >> 6;
-    int loc[4], gl4[4];
+    int loc[4];
     int run = 0;
     const int v4[4] = {pk.x, pk.y, pk.z, pk.w};
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
-        int c, g;
-        step_unpack(v4[e], &c, &g);
         loc[e] = run;
-        gl4[e] = g;
-        run += c;
+        run += v4[e] & 0xffff;
     }
     const int incl = wave_incl_sum(run);
     const int excl = incl - run;   // this thread's start within its wave
     // Prefixes grow with g and a goal child's in-block index is below its block's
-    // count, so the lowest g holding a goal child has the lowest global index.
+    // count, so the lowest g holding a goal child has the lowest global index.  Only a
+    // wave that holds a goal flag looks (none while the goal is out of reach or disabled).
     int gl = kNoGoalIdx;
+    if (__ballot(((pk.x | pk.y | pk.z | pk.w) >> 16) != 0) != 0ull) {
 #pragma unroll
-    for (int e = 3; e >= 0; --e)
-        if (gl4[e] >= 0) gl = excl + loc[e] + gl4[e];
-    gl = first_lane_value(gl != kNoGoalIdx, gl, kNoGoalIdx);
+        for (int e = 3; e >= 0; --e) {
+            int c, g;
+            step_unpack(v4[e], &c, &g);
+            if (g >= 0) gl = excl + loc[e] + g;
+        }
+        gl = first_lane_value(gl != kNoGoalIdx, gl, kNoGoalIdx);
+    }
     if (lane == kWave - 1) sRed[0][wave] = incl;
     if (lane == 0) sRed[1][wave] = gl;
     __syncthreads();
-    const int w0 = sRed[0][0], w1 = sRed[0][1], w2 = sRed[0][2], w3 = sRed[0][3];
-    // uniform by construction; readfirstlane so the plan that follows is scalar code
-    *A = __builtin_amdgcn_readfirstlane(w0 + w1 + w2 + w3);
-    const int g0 = sRed[1][0], g1 = sRed[1][1], g2 = sRed[1][2], g3 = sRed[1][3];
+    // uniform by construction; readfirstlane so that A, jGoal and the plan that follows
+    // are scalar code
+    const int w0 = __builtin_amdgcn_readfirstlane(sRed[0][0]), w1 = __builtin_amdgcn_readfirstlane(sRed[0][1]),
+              w2 = __builtin_amdgcn_readfirstlane(sRed[0][2]), w3 = __builtin_amdgcn_readfirstlane(sRed[0][3]);
+    *A = w0 + w1 + w2 + w3;
+    const int g0 = __builtin_amdgcn_readfirstlane(sRed[1][0]), g1 = __builtin_amdgcn_readfirstlane(sRed[1][1]),
+              g2 = __builtin_amdgcn_readfirstlane(sRed[1][2]), g3 = __builtin_amdgcn_readfirstlane(sRed[1][3]);
     int jg = kNoGoalIdx;   // the lowest wave holding one has the lowest index
     if (g3 != kNoGoalIdx) jg = w0 + w1 + w2 + g3;
     if (g2 != kNoGoalIdx) jg = w0 + w1 + g2;
     if (g1 != kNoGoalIdx) jg = w0 + g1;
     if (g0 != kNoGoalIdx) jg = g0;
-    *jGoal = __builtin_amdgcn_readfirstlane(jg);
+    *jGoal = jg;
     const int base = excl + (wave > 0 ? w0 : 0) + (wave > 1 ? w1 : 0) + (wave > 2 ? w2 : 0);
+    if (tid * 4 + 3 <= d.nBlocks) {   // one 16-B LDS store (sPfx is 16-B aligned)
+        *reinterpret_cast<int4*>(sPfx + tid * 4) = make_int4(base, base + loc[1], base + loc[2], base + loc[3]);
+    } else {
 #pragma unroll
-    for (int e = 0; e < 4; ++e)
-        if (tid * 4 + e <= d.nBlocks) sPfx[tid * 4 + e] = base + loc[e];
+        for (int e = 0; e < 4; ++e)
+            if (tid * 4 + e <= d.nBlocks) sPfx[tid * 4 + e] = base + loc[e];
+    }
     if (tid == kBlock - 1 && d.nBlocks == kMaxStepBlocks) sPfx[kMaxStepBlocks] = *A;
 }
 
@@ -1356,8 +1366,15 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) voi
     const int pp = (t - 1) & 1, cp = t & 1;
     const SBMP_GAS unsigned long long* const pubCur = G(d.stepPub) + (size_t)cp * (d.nR1 + nW);
     // d.timeline if this launch is the traced one (decided on the host: no dependent
-    // loads of the plan struct before the prologue's own)
+    // loads of the plan struct before the prologue's own).  Only a diagnostic build
+    // (SBMP_HIPCC_FLAGS=-DSBMP_TIMELINE, tools/_tl.sh) stamps: held in registers, the
+    // eight 64-bit stamps cost every wave ~30 VALU of zeroing and moves.
+#ifdef SBMP_TIMELINE
     long long* const tl = tlBase ? tlBase + ((size_t)b * (kBlock / kWave) + wave) * kTimelineStamps : nullptr;
+#else
+    long long* const tl = nullptr;
+    (void)tlBase;
+#endif
     long long stamp[kTimelineStamps] = {0, 0, 0, 0, 0, 0, 0, 0};
 #define SBMP_STAMP(i)                                                                  \
     do {                                                                               \
@@ -1559,12 +1576,17 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) voi
         fast = car_fast_ok(d);   // per plan (uniform)
         if (fast) {
             // a huge steering tan can drive theta past Cody-Waite's range within a child
-            if (__ballot(!car_theta_bounded(p, ctl, d)) == 0ull) valid = car_euler_fast<OBS, false>(p, ctl, d, obs, out) && act;
-            else valid = car_euler_fast<OBS, true>(p, ctl, d, obs, out) && act;
+            const WaveCull cull = car_cull<OBS>(p, ctl, d, obs);
+            if (__ballot(!car_theta_bounded(p, ctl, d)) == 0ull)
+                valid = car_euler_fast<OBS, false>(p, ctl, d, obs, cull, out) && act;
+            else
+                valid = car_euler_fast<OBS, true>(p, ctl, d, obs, cull, out) && act;
         }
     }
-    if (!fast && act)
-        valid = (AGENT == 0) ? car_euler<OBS>(p, ctl, d, obs, out) : point_euler<OBS>(p, ctl, d, obs, out);
+    if (!fast) {
+        out = ChildOut{};   // inactive lanes: defined values (the fast loop writes every lane)
+        if (act) valid = (AGENT == 0) ? car_euler<OBS>(p, ctl, d, obs, out) : point_euler<OBS>(p, ctl, d, obs, out);
+    }
     SBMP_STAMP(3);
 
     // ---- bins (KGMT.cu:390-391) and the accept test (KGMT.cu:394-411, D2)
@@ -1585,13 +1607,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) voi
         aw = pubCur[d.nR1 + (q2 >> 5)];
     }
     float u = 0.0f;
-    float4 cs = make_float4(0.f, 0.f, 0.f, 0.f), cc = cs;   // this slot's child (state, ctrl)
-    float cost = 0.0f;
+    if (valid) u = xorwow_uniform(rs);   // KGMT.cu:395 (valid implies act)
+    // this slot's child (state, ctrl); meaningless on inactive lanes, which store nothing
+    // (a stale flag past S re-reads its child below)
+    float4 cs = out.state;
+    float4 cc = make_float4(out.a, out.steer, out.dur, __int_as_float(parent));
+    float cost = parentCost + out.dur;   // getCost (KGMT.cu:631-633), as the insert computes it
     if (act) {
-        if (valid) u = xorwow_uniform(rs);   // KGMT.cu:395
-        cs = out.state;
-        cc = make_float4(out.a, out.steer, out.dur, __int_as_float(parent));
-        cost = parentCost + out.dur;   // getCost (KGMT.cu:631-633), as the insert computes it
         store_wt(d.uState, slot, cs);   // write-through: fewer dirty lines at the boundary
         store_wt(d.uCtrl, slot, cc);
         store_wt(d.rngA, slot, make_uint4(rs.v0, rs.v1, rs.v2, rs.v3));
@@ -1649,7 +1671,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) voi
         }
     }
     bool inGoal = false;
-    if (flagged) {
+    if (flagged && d.goalThreshold > 0.0f) {   // sqrtf(.) < r is false for every r <= 0 (and NaN)
         const float dx = cs.x - d.goalX, dy = cs.y - d.goalY;   // inGoalRegion, KGMT.cu:635-638
         inGoal = __builtin_sqrtf(dx * dx + dy * dy) < d.goalThreshold;
     }

@@ -11,6 +11,7 @@
 #include <algorithm>
 #include <chrono>
 #include <cmath>
+#include <cstdio>
 #include <cstring>
 #include <fstream>
 #include <iomanip>
@@ -283,6 +284,10 @@ KgmtPlanner::KgmtPlanner(const sbmp_kgmt_params& p, int nranks, int rank, Exchan
     d.timelineFin = nullptr;
     d.timelineIter = -1;
     if (const char* v = getenv("SBMP_TIMELINE_ITER")) {   // diagnostics: tools/timeline.py
+#ifndef SBMP_TIMELINE
+        fprintf(stderr, "sbmp: SBMP_TIMELINE_ITER set, but k_step stamps only in a build with "
+                        "SBMP_HIPCC_FLAGS=-DSBMP_TIMELINE (tools/_tl.sh); its expanding waves' stamps stay 0\n");
+#endif
         d.timelineIter = atoi(v);
         const size_t n = (size_t)expandBlocks_ * (kBlock / kWave) * kTimelineStamps;
         const size_t nf = (size_t)(1 + d.nBlocks) * kTimelineStamps;
