@@ -548,7 +548,12 @@ __device__ __forceinline__ WaveCull wave_cull(float x0, float y0, float rx, floa
         const sbmp_f32x2 lo = sbmp_f32x2{o.x, o.y} - mx;
         const sbmp_f32x2 hi = mn - sbmp_f32x2{o.z, o.w};
         const float sep = __builtin_fmaxf(vmax3(lo.x, lo.y, hi.x), hi.y);
-        if (__ballot(sep < 0.0f) != 0ull) w.boxes |= 1u << i;
+        // the flag from the ballot on the scalar unit (written as a select, the compiler
+        // kept the flags as lane booleans and merged them with vector ORs)
+        const unsigned long long m = __ballot(sep < 0.0f);
+        unsigned bit;
+        asm("s_cmp_lg_u64 %1, 0\n\ts_cselect_b32 %0, %2, 0" : "=s"(bit) : "s"(m), "s"(1u << i) : "scc");
+        w.boxes |= bit;
     }
     if (d.obsNaN) w.boxes = ~0u;
     return w;

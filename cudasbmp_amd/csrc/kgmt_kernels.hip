@@ -892,7 +892,7 @@ __device__ __forceinline__ void step_scan(const KgmtDev& d, int4 pk, int* sPfx, 
                                           int* jGoal) {
     const int tid = threadIdx.x;
     const int lane = tid & (kWave - 1);
-    const int wave = tid >> 6;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // uniform: scalar selects below
     int loc[4];
     int run = 0;
     const int v4[4] = {pk.x, pk.y, pk.z, pk.w};
@@ -1358,7 +1358,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) voi
     float4* const sObs = sDyn;
     const int tid = threadIdx.x;
     const int lane = tid & (kWave - 1);
-    const int wave = tid >> 6;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // uniform
+    __shared__ int2 sWaveDiv[kBlock / kWave];   // (frontier position, remainder) of each wave's first slot
     const int b = (int)blockIdx.x - 1;                // this workgroup's 256-slot block (owned index)
     const int gb = SH ? d.rank + d.nranks * b : b;   // global block
     const int slot = gb * kBlock + tid;
@@ -1443,6 +1444,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) voi
         if (wave == 0) {
             const StepPlan q0 = plan();
             if (lane == 0) sPlan = q0;
+            // slot = g k + i for the first slot of each wave, one division for all four
+            // (k >= 64: a wave's slots then span at most two frontier positions)
+            if (lane < kBlock / kWave && q0.k >= kWave) {
+                const int s0 = gb * kBlock + lane * kWave;
+                const int g0 = slot_div(d, s0, q0.k);
+                sWaveDiv[lane] = make_int2(g0, s0 - g0 * q0.k);
+            }
         }
         __syncthreads();
         q = uniform_plan(sPlan);
@@ -1452,7 +1460,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) voi
     // ---- D6 clear of this block's words of t-1 (KGMT.cu:231,556)
     const long long cleared = d.fixGNewClear ? (1ll << 62) : 32ll * q.grid;
     unsigned long long word = oldWord;
-    if (lane == 0) {
+    if (d.fixGNewClear) {   // the complete clear: every word (uniform branch)
+        word = 0ull;
+    } else if (lane == 0) {
         const long long wbase = (long long)(slot >> 6) * kWave;
         if (wbase + kWave <= cleared) word = 0ull;
         else if (wbase < cleared) word = oldWord & ~((1ull << (cleared - wbase)) - 1ull);
@@ -1499,7 +1509,14 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) voi
 
     // ---- expand t
     const bool act = slot < q.S;
-    const int g = !act ? 0 : slot_div(d, slot, q.k);   // slot = g*k + i
+    int g;   // slot = g*k + i
+    if (!SH && q.k >= kWave) {
+        const int2 gr = sWaveDiv[wave];
+        g = gr.x + ((gr.y + lane >= q.k) ? 1 : 0);
+    } else {
+        g = slot_div(d, slot, q.k);
+    }
+    g = act ? g : 0;
     const int parent = act ? q.gLo + g : 0;
     const SBMP_GAS float4* src = G(d.treeState) + parent;   // the parent's state, and its cost
     const SBMP_GAS float* srcCost = &G(d.treeCtrl)[parent].w;
@@ -1663,7 +1680,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) voi
         (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)word, 0);
     const unsigned long long wordAll = word0 | mask;   // GNew |= accept (stale bits survive)
     const bool flagged = (wordAll >> lane) & 1ull;
-    if (__ballot(flagged && !act) != 0ull) {   // rare; keeps the wait below off the common path
+    if ((wordAll & ~__ballot(act)) != 0ull) {   // rare; keeps the wait below off the common path
         if (flagged && !act) {   // a stale flag on a slot past S: the child last written there
             cs = G(d.uState)[slot];
             cc = G(d.uCtrl)[slot];
@@ -1676,7 +1693,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) voi
         inGoal = __builtin_sqrtf(dx * dx + dy * dy) < d.goalThreshold;
     }
     // index among the wave's flagged slots; the first goal child is the wave's lowest
-    const int idxW = __popcll(wordAll & ((1ull << lane) - 1ull));
+    const int idxW = __builtin_amdgcn_mbcnt_hi((uint32_t)(wordAll >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)wordAll, 0u));
     const int glW = first_lane_value(flagged && inGoal, idxW, kNoGoalIdx);
     if (lane == 0) {
         G(d.gnewOut)[slot >> 6] = wordAll;
