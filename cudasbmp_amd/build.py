@@ -33,6 +33,9 @@ COMMON = [
     # 16-bit integer vectors (~25 extra VALU per step); float pairs that should be
     # packed are written as float2 by hand (kgmt_device.h sincos_poly2).
     "-fno-slp-vectorize",
+    # The first 16 kernel-argument dwords arrive preloaded in SGPRs (gfx950): k_step's
+    # first loads issue without a scalar round trip to the kernel-argument segment.
+    "-mllvm", "-amdgpu-kernarg-preload-count=16",
     f"--offload-arch={ARCH}",
     "-I", os.path.join(ROOT, "include"), "-I", CSRC,
     "-Wall", "-Wno-unused-result",

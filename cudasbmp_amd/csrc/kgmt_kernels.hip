@@ -1334,9 +1334,18 @@ __device__ __forceinline__ void step_planner(const KgmtDev& d, int t, int expand
 // counts, R1 deltas and R2New of t-1 come from the exchange (stepXr), this launch's
 // go to stepXs[t & 1]; the flagged children's lists are the record buffers, and
 // workgroup b inserts t-1's children of blocks b P .. b P + P - 1 (one of each rank).
+// The arguments the prologue's first loads need come first: the build preloads the
+// first 16 argument dwords into SGPRs (-amdgpu-kernarg-preload-count, build.py), so
+// those loads issue at wave start instead of behind two dependent scalar loads
+// (kernel argument -> plan struct -> pointer).
+// (14 dwords: the kernel-argument segment pointer takes two of the 16 user SGPRs)
+//   cnt4     t-1's packed counts (parity (t-1) & 1 of stepCnt; sharded: the exchange's rows)
+//   ctrlPrev ctrl[t-1]
 template <int AGENT, int OBS, bool SH>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) void k_step(
-    const KgmtDev* __restrict__ dp, int t, int expand, long long* tlBase) {
+    const KgmtDev* __restrict__ dp, int t, int expand, const int4* __restrict__ cnt4,
+    const IterCtrl* __restrict__ ctrlPrev, const uint4* __restrict__ rngAArg, const uint2* __restrict__ rngBArg,
+    const unsigned long long* __restrict__ gnewArg, const PlannerStatus* __restrict__ statusArg, long long* tlBase) {
     const KgmtDev& d = *dp;
     extern __shared__ float4 sDyn[];   // [LDS obstacles][prefix: nBlocks + 1 ints][R2New bits: nR2 / 32]
     __shared__ int sR1P[kMaxR1];
@@ -1381,32 +1390,29 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) voi
     do {                                                                               \
         if (tl) stamp[i] = (long long)__builtin_amdgcn_s_memrealtime();                \
     } while (0)
-    // The prologue's pointers in one batch of scalar loads (one round trip; loaded
-    // where first used they were five dependent ones)
-    const SBMP_GAS int* const cntP = G(d.stepCnt);
-    const SBMP_GAS IterCtrl* const ctrlP = G(d.ctrl);
-    const SBMP_GAS PlannerStatus* const statusP = G(d.status);
-    const SBMP_GAS uint4* const rngAP = G(d.rngA);
-    const SBMP_GAS uint2* const rngBP = G(d.rngB);
-    const SBMP_GAS unsigned long long* const gnewP = G(d.gnewOut);
-    // (with the plan's scalars from the first 64 B of the struct)
-    asm volatile("" ::"s"(cntP), "s"(ctrlP), "s"(statusP), "s"(rngAP), "s"(rngBP), "s"(gnewP), "s"(d.M),
-                 "s"(d.nBlocks), "s"(d.numIterations), "s"(d.numDisc), "s"(d.nR1), "s"(d.nR2), "s"(d.cap),
-                 "s"(d.fixGNewClear), "s"(d.batchRule), "s"(d.rcpNumDisc), "s"(d.treeState), "s"(d.treeCtrl),
-                 "s"(d.stepList));
+    // The first loads' pointers are preloaded arguments; the plan's scalars and the
+    // next pointers in one batch of scalar loads from the struct (one round trip, in
+    // flight with the vector loads below)
+    const SBMP_GAS IterCtrl* const ctrlP = G(ctrlPrev);
+    const SBMP_GAS PlannerStatus* const statusP = G(statusArg);
+    const SBMP_GAS uint4* const rngAP = G(rngAArg);
+    const SBMP_GAS uint2* const rngBP = G(rngBArg);
+    const SBMP_GAS unsigned long long* const gnewP = G(gnewArg);
     SBMP_STAMP(0);
 
     // ---- loads that depend on nothing else (the control block as a plain load: a
     // waiting scalar load would serialise behind the scan)
-    const int4 pk = SH ? reinterpret_cast<const SBMP_GAS int4*>(G(d.stepXr) + d.xRowOff)[tid]
-                       : *reinterpret_cast<const SBMP_GAS int4*>(cntP + (size_t)pp * kMaxStepBlocks + tid * 4);
-    const IterCtrl pc = ctrlP[t - 1];
+    const int4 pk = G(cnt4)[tid];
+    const IterCtrl pc = *ctrlP;
     int rowW[SH ? kMaxRanks : 1];   // sharded: the block words of this workgroup's row (its inserts)
     if constexpr (SH) row_words(d, b, rowW);
     const int goalIdx = statusP->goalIdx;
     const uint4 ra = rngAP[slot];
     const uint2 rb = rngBP[slot];
     const unsigned long long oldWord = (lane == 0) ? gnewP[slot >> 6] : 0ull;
+    asm volatile("" ::"s"(d.M), "s"(d.nBlocks), "s"(d.numIterations), "s"(d.numDisc), "s"(d.nR1), "s"(d.nR2),
+                 "s"(d.cap), "s"(d.fixGNewClear), "s"(d.batchRule), "s"(d.rcpNumDisc), "s"(d.treeState),
+                 "s"(d.treeCtrl), "s"(d.stepList));
     float4 obsReg = make_float4(0.f, 0.f, 0.f, 0.f);
     if (kLdsObs && tid < d.nObs) obsReg = G(d.obstacles)[tid];
     sR1P[tid] = 0;   // nR1 == kBlock
@@ -1952,27 +1958,31 @@ static void launch_step_form(const KgmtDev& d, int t, int expand, int variant, h
     const int blocks = SH ? d.nBlocks / d.nranks : d.nBlocks;
     const dim3 grid(1 + blocks), block(kBlock);   // workgroup 0 plans, 1.. expand
     long long* const tlBase = (!SH && d.timeline && t == d.timelineIter && expand) ? d.timeline : nullptr;
+    const int4* const cnt4 = SH ? reinterpret_cast<const int4*>(d.stepXr + d.xRowOff)
+                                : reinterpret_cast<const int4*>(d.stepCnt + (size_t)((t - 1) & 1) * kMaxStepBlocks);
+#define SBMP_STEP_ARGS d.devSelf, t, expand, cnt4, d.ctrl + (t - 1), d.rngA, d.rngB, d.gnewOut, d.status, tlBase
     if (d.gridStart) {
-        launch(k_step<AGENT, kObsGrid, SH>, grid, block, pfx, s, tm, d.devSelf, t, expand, tlBase);
+        launch(k_step<AGENT, kObsGrid, SH>, grid, block, pfx, s, tm, SBMP_STEP_ARGS);
     } else if (d.nObs > kMaxLdsObs) {
-        launch(k_step<AGENT, kObsGlobal, SH>, grid, block, pfx, s, tm, d.devSelf, t, expand, tlBase);
+        launch(k_step<AGENT, kObsGlobal, SH>, grid, block, pfx, s, tm, SBMP_STEP_ARGS);
     } else if (d.nObs <= kMaxRegObs && (variant == 0 || variant == 3)) {
         switch (d.nObs) {
-            case 0: launch(k_step<AGENT, kObsReg + 0, SH>, grid, block, pfx, s, tm, d.devSelf, t, expand, tlBase); break;
-            case 1: launch(k_step<AGENT, kObsReg + 1, SH>, grid, block, pfx, s, tm, d.devSelf, t, expand, tlBase); break;
-            case 2: launch(k_step<AGENT, kObsReg + 2, SH>, grid, block, pfx, s, tm, d.devSelf, t, expand, tlBase); break;
-            case 3: launch(k_step<AGENT, kObsReg + 3, SH>, grid, block, pfx, s, tm, d.devSelf, t, expand, tlBase); break;
-            case 4: launch(k_step<AGENT, kObsReg + 4, SH>, grid, block, pfx, s, tm, d.devSelf, t, expand, tlBase); break;
-            case 5: launch(k_step<AGENT, kObsReg + 5, SH>, grid, block, pfx, s, tm, d.devSelf, t, expand, tlBase); break;
-            case 6: launch(k_step<AGENT, kObsReg + 6, SH>, grid, block, pfx, s, tm, d.devSelf, t, expand, tlBase); break;
-            case 7: launch(k_step<AGENT, kObsReg + 7, SH>, grid, block, pfx, s, tm, d.devSelf, t, expand, tlBase); break;
-            default: launch(k_step<AGENT, kObsReg + 8, SH>, grid, block, pfx, s, tm, d.devSelf, t, expand, tlBase); break;
+            case 0: launch(k_step<AGENT, kObsReg + 0, SH>, grid, block, pfx, s, tm, SBMP_STEP_ARGS); break;
+            case 1: launch(k_step<AGENT, kObsReg + 1, SH>, grid, block, pfx, s, tm, SBMP_STEP_ARGS); break;
+            case 2: launch(k_step<AGENT, kObsReg + 2, SH>, grid, block, pfx, s, tm, SBMP_STEP_ARGS); break;
+            case 3: launch(k_step<AGENT, kObsReg + 3, SH>, grid, block, pfx, s, tm, SBMP_STEP_ARGS); break;
+            case 4: launch(k_step<AGENT, kObsReg + 4, SH>, grid, block, pfx, s, tm, SBMP_STEP_ARGS); break;
+            case 5: launch(k_step<AGENT, kObsReg + 5, SH>, grid, block, pfx, s, tm, SBMP_STEP_ARGS); break;
+            case 6: launch(k_step<AGENT, kObsReg + 6, SH>, grid, block, pfx, s, tm, SBMP_STEP_ARGS); break;
+            case 7: launch(k_step<AGENT, kObsReg + 7, SH>, grid, block, pfx, s, tm, SBMP_STEP_ARGS); break;
+            default: launch(k_step<AGENT, kObsReg + 8, SH>, grid, block, pfx, s, tm, SBMP_STEP_ARGS); break;
         }
     } else if (variant == 2) {
-        launch(k_step<AGENT, kObsLds4, SH>, grid, block, shm, s, tm, d.devSelf, t, expand, tlBase);
+        launch(k_step<AGENT, kObsLds4, SH>, grid, block, shm, s, tm, SBMP_STEP_ARGS);
     } else {
-        launch(k_step<AGENT, kObsLds, SH>, grid, block, shm, s, tm, d.devSelf, t, expand, tlBase);
+        launch(k_step<AGENT, kObsLds, SH>, grid, block, shm, s, tm, SBMP_STEP_ARGS);
     }
+#undef SBMP_STEP_ARGS
 }
 
 template <int AGENT>
