@@ -1549,12 +1549,19 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) voi
             m = __ballot((idx < nS ? sPfx[idx] : INT_MAX) <= jj);
             lo = (j == jA) ? cA * 32 + __popcll(m & 0xffffffffull) - 1 : cB * 32 + __popcll(m >> 32) - 1;
         } else {
-            int hi = nS;
-            while (hi - lo > 1) {
-                const int mid = (lo + hi) >> 1;
-                if (sPfx[mid] <= j) lo = mid;
-                else hi = mid;
-            }
+            // k < 64: the wave's positions jA .. jB are consecutive and span a couple of
+            // blocks (a block holds A / nBlocks > 4 of them on average), so the block of jA
+            // by the same 32-ary ballot search, then each lane steps forward (was a
+            // 10-step binary search per lane: iterations 2-10 of the c3 window)
+            const int sub = lane & 31;
+            int idx = sub * 32;
+            unsigned long long m = __ballot((idx < nS ? sPfx[idx] : INT_MAX) <= jA);
+            const int c = __popcll(m & 0xffffffffull) - 1;
+            idx = c * 32 + sub;
+            m = __ballot((idx < nS ? sPfx[idx] : INT_MAX) <= jA);
+            lo = c * 32 + __popcll(m & 0xffffffffull) - 1;
+            if (fromList)
+                while (lo + 1 < nS && sPfx[lo + 1] <= j) ++lo;
         }
         if (fromList) {
             if constexpr (SH) {   // the row's blocks: one more (L2) round trip for their words
