@@ -321,8 +321,61 @@ KgmtPlanner::KgmtPlanner(const sbmp_kgmt_params& p, int nranks, int rank, Exchan
             ex_->share_buffer(own, sizeof(unsigned long long) * words, ib);
             for (int q = 0; q < nranks; ++q) inbox_[q] = static_cast<unsigned long long*>(ib[q]);
             oneshot_ = true;
+            if (!oneshot_self_test()) {
+                oneshot_ = false;   // on every rank: the verdict is all-reduced
+                fprintf(stderr, "sbmp: rank %d: the one-shot exchange failed its start-up check on this machine; "
+                                "the per-iteration exchange is the communicator's all-reduce\n", rank);
+            }
         }
     }
+}
+
+// The one-shot exchange checked once on this machine before an iteration relies on it:
+// two exchanges (both inbox parities) of rank-specific words through k_oneshot, the sums
+// compared on the host.  A wrong word or a timed-out peer flag on any rank (the verdicts
+// are summed with the communicator's all-reduce) makes every rank use that all-reduce
+// instead, so a fabric on which the inboxes' system-scope stores and flags misbehave costs
+// speed, not a wrong or stalled run.  Runs in the constructor, where the collective IPC
+// handle exchange has just lined the ranks up.
+static unsigned long long oneshot_pattern(int rank, size_t i, int pass) {
+    return ((unsigned long long)(rank + 1) * 0x9E3779B97F4A7C15ull) ^ ((unsigned long long)i * 0x100000001ull + pass);
+}
+
+bool KgmtPlanner::oneshot_self_test() {
+    const size_t n = xWords_;
+    const int P = d_.nranks;
+    std::vector<unsigned long long> h(n), got(n);
+    unsigned long long* send = alloc<unsigned long long>(n);
+    unsigned long long* verdict = alloc<unsigned long long>(2);
+    int error = 0;
+    SBMP_HIP(hipMemsetAsync(&d_.status->error, 0, sizeof(int), stream_));
+    bool ok = true;
+    for (int pass = 0; pass < 2; ++pass) {
+        for (size_t i = 0; i < n; ++i) h[i] = oneshot_pattern(d_.rank, i, pass);
+        SBMP_HIP(hipMemcpyAsync(send, h.data(), sizeof(unsigned long long) * n, hipMemcpyHostToDevice, stream_));
+        ++xSeq_;
+        launch_oneshot(inbox_, send, xRecv_, (long long)n, P, d_.rank, xSeq_, &d_.status->error, stream_,
+                       KernelTiming{});
+        SBMP_HIP(hipMemcpyAsync(got.data(), xRecv_, sizeof(unsigned long long) * n, hipMemcpyDeviceToHost, stream_));
+        SBMP_HIP(hipMemcpyAsync(&error, &d_.status->error, sizeof(int), hipMemcpyDeviceToHost, stream_));
+        SBMP_HIP(hipStreamSynchronize(stream_));
+        if (error) ok = false;
+        for (size_t i = 0; i < n && ok; ++i) {
+            unsigned long long want = 0;
+            for (int q = 0; q < P; ++q) want += oneshot_pattern(q, i, pass);
+            if (got[i] != want) ok = false;
+        }
+    }
+    SBMP_HIP(hipMemsetAsync(&d_.status->error, 0, sizeof(int), stream_));
+    if (const char* f = getenv("SBMP_ONESHOT_SELFTEST"))   // tests: this rank reports a failure
+        if (std::string(f) == "fail") ok = false;
+    const unsigned long long bad = ok ? 0ull : 1ull;
+    SBMP_HIP(hipMemcpyAsync(verdict, &bad, sizeof(bad), hipMemcpyHostToDevice, stream_));
+    ex_->allreduce_u64(verdict, verdict + 1, 1, stream_);
+    unsigned long long anyBad = 0;
+    SBMP_HIP(hipMemcpyAsync(&anyBad, verdict + 1, sizeof(anyBad), hipMemcpyDeviceToHost, stream_));
+    SBMP_HIP(hipStreamSynchronize(stream_));
+    return anyBad == 0;
 }
 
 KgmtPlanner::~KgmtPlanner() {

@@ -195,6 +195,7 @@ private:
     unsigned long long* xRecv_ = nullptr;
     size_t xWords_ = 0;
     bool oneshot_ = false;                   // sharded: the exchange is k_oneshot over IPC-mapped inboxes
+    bool oneshot_self_test();                // k_oneshot checked once at construction (all ranks agree)
     unsigned long long* inbox_[kMaxRanks] = {nullptr};
     unsigned long long xSeq_ = 0;            // exchanges so far (the same count on every rank)
     uint32_t* jumps_ = nullptr;

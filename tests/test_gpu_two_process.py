@@ -41,6 +41,10 @@ def _rank_main(rank, port, kw, seed, out_dir, exchange, delay=0.0):
         os.environ["SBMP_EXCHANGE"] = exchange
     else:
         os.environ.pop("SBMP_EXCHANGE", None)
+    if exchange == "oneshot-check-fails" and rank == 1:   # only rank 1's start-up check "fails"
+        os.environ["SBMP_ONESHOT_SELFTEST"] = "fail"
+    else:
+        os.environ.pop("SBMP_ONESHOT_SELFTEST", None)
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     import torch.distributed as dist
@@ -55,14 +59,16 @@ def _rank_main(rank, port, kw, seed, out_dir, exchange, delay=0.0):
     g = KGMT(**cfg, **extra, _host_sharded=(TorchCollectives(dist), WORLD, rank))
     if rank == 1 and delay:
         time.sleep(delay)   # process skew before the first exchange (begin() holds a host barrier)
+    g.set_profiling(True)   # counts the launches: which exchange ran
     r = g.plan(DEMO_INITIAL, DEMO_GOAL, DeviceBuffer(obs), len(obs), seed=seed)
+    oneshots = g.kernel_stats().get("k_oneshot", (0, 0.0))[0]
     s, p, c = g.tree()
     G, GN = g.flags()          # GNew words live with their owner: merged by the all-reduce
     reg = g.regions()          # R2Valid / R2Invalid: each rank folded its own children
     u, up = g.unexplored()     # slots of other ranks read as 0 / -1
     rng = g.rng()
     np.savez(os.path.join(out_dir, f"rank{rank}.npz"), s=s, p=p, c=c, G=G, GN=GN, u=u, up=up, rng=rng,
-             log=g.iter_log(), res=np.array([r.iterations, r.treeSize, r.goalIndex]),
+             log=g.iter_log(), res=np.array([r.iterations, r.treeSize, r.goalIndex]), oneshots=oneshots,
              cost=np.float32(r.costToGoal), **{"reg_" + k: v for k, v in reg.items()})
     g.close()
     dist.destroy_process_group()
@@ -79,6 +85,10 @@ def _rank_main(rank, port, kw, seed, out_dir, exchange, delay=0.0):
     # rank 1 starts 3 s late (round 2's exchange gave up after 1 s)
     (dict(samplesPerIteration=4096, batchRule="fill", maxTreeSize=200000, numIterations=15, goalThreshold=0.0), 21,
      "oneshot", 3.0),
+    # rank 1's start-up check of the one-shot exchange fails: both ranks must switch to the
+    # all-reduce together (one rank alone would leave the other waiting for its flags)
+    (dict(samplesPerIteration=4096, batchRule="fill", maxTreeSize=200000, numIterations=15, goalThreshold=0.0), 21,
+     "oneshot-check-fails", 0.0),
 ])
 def test_two_processes_one_gpu_bit_exact(kw, seed, exchange, delay, tmp_path, obstacles, oracle_lib):
     ctx = mp.get_context("spawn")
@@ -108,6 +118,11 @@ def test_two_processes_one_gpu_bit_exact(kw, seed, exchange, delay, tmp_path, ob
     info = o.info()
     n = o.rng().shape[0]
     owner = (np.arange(n) // 256) % WORLD
+    for r, d in enumerate(R):
+        if exchange == "oneshot":
+            assert int(d["oneshots"]) > 0, f"rank {r}: the one-shot exchange did not run"
+        else:
+            assert int(d["oneshots"]) == 0, f"rank {r}: k_oneshot ran ({int(d['oneshots'])} launches)"
     for r, d in enumerate(R):   # every rank holds the whole tree and the merged exports
         assert np.array_equal(d["log"], o.iter_logs()), f"rank {r}: iteration logs differ"
         assert np.array_equal(d["p"], po), f"rank {r}: parents differ"
