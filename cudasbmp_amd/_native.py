@@ -87,6 +87,11 @@ class InsertBatchArgs(ctypes.Structure):   # sbmp_insert_batch_args
                 ("fixGNewClear", ctypes.c_int), ("inserted", ctypes.c_void_p), ("goalIndex", ctypes.c_void_p)]
 
 
+class PathInfo(ctypes.Structure):   # sbmp_path_info
+    _fields_ = [(n, ctypes.c_int) for n in ("stepForm", "obstacleForm", "residentGroups", "neededGroups", "exchange",
+                                            "nranks", "rank", "commRanks")]
+
+
 class KernelStat(ctypes.Structure):
     _fields_ = [("name", ctypes.c_char * 32), ("launches", ctypes.c_longlong), ("totalMs", ctypes.c_double)]
 
@@ -97,7 +102,7 @@ EXPORTED_SYMBOLS = (
     "sbmp_kgmt_create", "sbmp_kgmt_destroy", "sbmp_kgmt_plan", "sbmp_kgmt_begin", "sbmp_kgmt_step",
     "sbmp_kgmt_enqueue", "sbmp_kgmt_sync", "sbmp_kgmt_fold", "sbmp_kgmt_result", "sbmp_kgmt_stream", "sbmp_kgmt_copy_tree",
     "sbmp_kgmt_copy_unexplored", "sbmp_kgmt_copy_flags", "sbmp_kgmt_copy_regions", "sbmp_kgmt_num_slots",
-    "sbmp_kgmt_copy_rng", "sbmp_kgmt_iter_log", "sbmp_kgmt_export_csv", "sbmp_kgmt_kernel_stats",
+    "sbmp_kgmt_copy_rng", "sbmp_kgmt_iter_log", "sbmp_kgmt_export_csv", "sbmp_kgmt_kernel_stats", "sbmp_kgmt_path_info",
     "sbmp_kgmt_reset_kernel_stats", "sbmp_kgmt_set_profiling", "sbmp_kgmt_kernel_samples", "sbmp_kgmt_enqueue_delay",
     "sbmp_read_obstacles_csv", "sbmp_device_upload_f32", "sbmp_device_free",
     "sbmp_device_count", "sbmp_comm_get_unique_id", "sbmp_kgmt_create_sharded", "sbmp_kgmt_create_local_group",
@@ -161,6 +166,7 @@ def lib():
         "sbmp_kgmt_export_csv": [vp, ctypes.c_char_p],
         "sbmp_kgmt_set_iteration_dump": [vp, ctypes.c_char_p],
         "sbmp_kgmt_kernel_stats": [vp, vp, i, P(i)],
+        "sbmp_kgmt_path_info": [vp, vp],
         "sbmp_kgmt_reset_kernel_stats": [vp],
         "sbmp_kgmt_set_profiling": [vp, i],
         "sbmp_kgmt_kernel_samples": [vp, ctypes.c_char_p, vp, i, P(i)],

@@ -110,6 +110,7 @@ struct KgmtDev {
     float width, height, agentLength, invAgentLength, goalThreshold, R1Size, R2Size, goalX, goalY;
     // RN(1/b) for div_by when the host verified it for this b (planner.cpp markstein_rcp), else 0
     float rcpR1Size, rcpR2Size, rcpNumDisc, rcpAgentLength;
+    float reachStep;   // 1.06 / numDisc: a bound on dt (duration <= 1.05) for car_schedule
     float4* treeState;
     float4* treeCtrl;
     int* treeParent;
@@ -232,16 +233,26 @@ constexpr int kBufferDword3 = 0x00020000;   // raw-buffer V# word 3 for gfx9 (ck
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t wt_rsrc(const void* base) {
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, 0x7fffffff, kBufferDword3);
 }
+// Offsets as (voffset, soffset).  soffset stays 0: ROCm 7.2's hazard recognizer does not pad
+// a MUBUF store whose soffset is an SGPR (tools/isa_hazards.py scans the
+// built library).  SBMP_SOFFSET_DEMO is that form (the slot's uniform block part in an
+// SGPR, valid for i = block * kBlock + threadIdx.x), kept only so tests/test_isa_hazards.py
+// can show that the scan catches it.
+#ifdef SBMP_SOFFSET_DEMO
+#define SBMP_WT_OFF(i, sz) ((i) & (kBlock - 1)) * (sz), __builtin_amdgcn_readfirstlane(((i) / kBlock) * kBlock * (sz))
+#else
+#define SBMP_WT_OFF(i, sz) (i) * (sz), 0
+#endif
 __device__ __forceinline__ void store_wt(float4* base, int i, float4 v) {
     __builtin_amdgcn_raw_buffer_store_b128(
         sbmp_u32x4{__float_as_uint(v.x), __float_as_uint(v.y), __float_as_uint(v.z), __float_as_uint(v.w)},
-        wt_rsrc(base), i * 16, 0, kCpolSc1);
+        wt_rsrc(base), SBMP_WT_OFF(i, 16), kCpolSc1);
 }
 __device__ __forceinline__ void store_wt(uint4* base, int i, uint4 v) {
-    __builtin_amdgcn_raw_buffer_store_b128(sbmp_u32x4{v.x, v.y, v.z, v.w}, wt_rsrc(base), i * 16, 0, kCpolSc1);
+    __builtin_amdgcn_raw_buffer_store_b128(sbmp_u32x4{v.x, v.y, v.z, v.w}, wt_rsrc(base), SBMP_WT_OFF(i, 16), kCpolSc1);
 }
 __device__ __forceinline__ void store_wt(uint2* base, int i, uint2 v) {
-    __builtin_amdgcn_raw_buffer_store_b64(sbmp_u32x2{v.x, v.y}, wt_rsrc(base), i * 8, 0, kCpolSc1);
+    __builtin_amdgcn_raw_buffer_store_b64(sbmp_u32x2{v.x, v.y}, wt_rsrc(base), SBMP_WT_OFF(i, 8), kCpolSc1);
 }
 
 // Slot i's XORWOW state for i < n, zeros with no memory access for i >= n: the
@@ -578,7 +589,8 @@ __device__ __forceinline__ bool motion_valid_culled(float minx, float miny, floa
 // Exec-masked instead of the reference's per-lane break: a dead lane skips the
 // step body (the wave keeps iterating while any lane is alive); a lane that fails
 // the bounds test keeps its new (x, y) and its old (theta, v), a lane that fails the
-// collision test keeps all four -- exactly the state at the reference's break.
+// collision test keeps the step's new (x, y, theta, v) -- exactly the state at the
+// reference's break (statePropagator.cu:42-45, 61-64).
 // Loop-invariant divisions by numDisc / agentLength use div_by when the host
 // verified the reciprocal (bit-exact; tools/check_fast_division.c).
 struct NoMidHook {
@@ -782,21 +794,88 @@ __device__ __forceinline__ WaveCull car_cull(float4 p, const ChildCtl& ctl, cons
     return wave_cull<OBS>(p.x, p.y, r, r, obs, d);
 }
 
+// Per-step cull of car_euler_fast, in place of wave_cull for most waves.  wave_cull
+// bounds a child's whole reach; the segment of Euler step i ends within r(t) = t |v0| +
+// |a| t^2 / 2 of the parent at t = (i + 1) dt, and the controls bound dt <= 1.05 / numDisc
+// and |a| <= 5 (statePropagator.cu:17-21: a = 10 u - 5, duration = u + 0.05, u in (0, 1]).
+// When the wave's active lanes expand at most two parents (consecutive rows: k >= 64,
+// where a steady-state wave holds one or two), box k cannot be met at step i by any lane
+// if its L-inf distance from the parents' bounding box is at least that bound for t =
+// (i + 1) reachStep (reachStep = 1.06 / numDisc, with wave_cull's margins), and the
+// workspace test of step i cannot fail if the square of that half-width around the box
+// lies inside the workspace.  One ballot decides every (step, box) pair and every step's
+// workspace test: lane L < NOBS D is the pair (L / NOBS, L % NOBS), lane NOBS D + i the
+// workspace test of step i.  Early steps of a long reach then skip the tests the whole-
+// child cull keeps (the parents move fast: a wave's reach spans half the workspace).
+// At the last step the bound covers every lane's whole reach (T <= 1.05), so the
+// schedule subsumes wave_cull, which runs only for waves it does not cover.
+// Inactive lanes' results are dropped, so only active lanes' parents count.
+struct StepSched {
+    unsigned long long boxes;    // bit i NOBS + k: box k may be met at step i
+    unsigned long long bounds;   // bit i: the workspace test of step i may fail
+    int shBoxes, shBounds;       // shift per step (0: no schedule, every step keeps the cull's set)
+    bool valid;                  // the schedule covers this wave (else wave_cull's set at every step)
+};
+
+__device__ __forceinline__ float lanef(float v, int l) {
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
+}
+
+// oLane: box (lane % NOBS) of the register list.
+template <int OBS>
+__device__ __forceinline__ StepSched car_schedule(float4 p, int parent, bool act, const KgmtDev& d, float4 oLane) {
+    constexpr int NOBS = obs_in_registers(OBS);
+    StepSched s{~0ull, ~0ull, 0, 0, false};
+    const int D = d.numDisc;
+    const unsigned long long am = __ballot(act);
+    if (am == 0ull || (NOBS + 1) * D > 64) return s;   // uniform
+    const int l0 = (int)__builtin_ctzll(am), l1 = 63 - (int)__builtin_clzll(am);
+    if (__builtin_amdgcn_readlane(parent, l1) - __builtin_amdgcn_readlane(parent, l0) > 1) return s;
+    const float x0 = lanef(p.x, l0), y0 = lanef(p.y, l0), x1 = lanef(p.x, l1), y1 = lanef(p.y, l1);
+    // (seg_min / seg_max: no canonicalising v_max per operand; finite states, D15)
+    const float v = seg_max(__builtin_fabsf(lanef(p.w, l0)), __builtin_fabsf(lanef(p.w, l1)));
+    const float xlo = seg_min(x0, x1), xhi = seg_max(x0, x1);
+    const float ylo = seg_min(y0, y1), yhi = seg_max(y0, y1);
+    const int L = (int)(threadIdx.x & (kWave - 1));
+    const int nb = NOBS * D;
+    const int i = (L < nb) ? L / (NOBS > 0 ? NOBS : 1) : L - nb;   // this lane's step
+    const float t = (float)(i + 1) * d.reachStep;
+    const float r = __builtin_fmaf(__builtin_fmaf(t, v, 2.5f * t * t), 1.0001f, 1e-3f);
+    // box item: L-inf distance of the lane's box from the parents' bounding box
+    const float db = __builtin_fmaxf(__builtin_fmaxf(oLane.x - xhi, xlo - oLane.z), __builtin_fmaxf(oLane.y - yhi, ylo - oLane.w));
+    // workspace item: the box's distance to the workspace's edges (uniform)
+    const float dw = __builtin_fminf(__builtin_fminf(xlo, ylo), __builtin_fminf(d.width - xhi, d.height - yhi));
+    const bool isBox = L < nb;   // bitwise, no branch: both items are computed on every lane
+    const bool may = (isBox & !(db >= r)) | (!isBox & (L < nb + D) & !(dw > r));
+    const unsigned long long m = __ballot(may);
+    s.boxes = m;
+    s.bounds = m >> nb;
+    s.shBoxes = NOBS;
+    s.shBounds = 1;
+    s.valid = true;
+    return s;
+}
+
 template <int OBS, bool PH>
 __device__ __forceinline__ bool car_euler_fast(float4 p, const ChildCtl& ctl, const KgmtDev& d, const float4* obs,
-                                               const WaveCull& cull, ChildOut& out) {
+                                               const WaveCull& cull, const StepSched& sched, ChildOut& out) {
     constexpr int NOBS = obs_in_registers(OBS);
     const float a = ctl.a, T = ctl.dur, dt = ctl.dt;
     // (v, theta): v in the low half, so the packed products broadcast it without a copy
     sbmp_f32x2 xy = {p.x, p.y}, vt = {p.w, p.z};
     const sbmp_f32x2 dt2 = {dt, dt}, wh = {d.width, d.height};
     const float invL = d.invAgentLength;
-    unsigned kept = __builtin_amdgcn_readfirstlane(cull.boxes);   // wave-uniform (a ballot)
+    const unsigned kept = __builtin_amdgcn_readfirstlane(cull.boxes);   // wave-uniform (a ballot)
+    unsigned long long sb = sched.boxes, sw = cull.bounds ? sched.bounds : 0ull;   // uniform
     float aliveF = 1.0f;   // 1 alive, 0 ended: a float, so no lane mask is carried across steps
     for (int i = 0; i < d.numDisc; ++i) {
         // re-tested every step (s_bitcmp1 + branch): hoisted, each kept flag would hold
         // a 64-bit lane mask in scalar registers for the whole loop
-        if (NOBS > 1) asm volatile("" : "+s"(kept));   // (one box: a single flag either way)
+        unsigned keptNow = kept & (unsigned)sb;
+        if (NOBS > 1) asm volatile("" : "+s"(keptNow));   // (one box: a single flag either way)
+        const bool bnd = (sw & 1ull) != 0ull;
+        sb >>= sched.shBoxes;
+        sw >>= sched.shBounds;
         float st, ct;
         if constexpr (PH) sincos_pred(vt.y, &st, &ct);   // Payne-Hanek for the rare lane past 105615
         else sincos_cw(vt.y, &st, &ct);
@@ -805,17 +884,17 @@ __device__ __forceinline__ bool car_euler_fast(float4 p, const ChildCtl& ctl, co
         const float vl = vt.x * invL;     // v / L, exact for a power-of-two L
         const sbmp_f32x2 nvt = __builtin_elementwise_fma(sbmp_f32x2{a, vl * ctl.tanS}, dt2, vt);
         float sep = 1.0f;   // >= 0: free of every kept box
-        if (kept) {
+        if (keptNow) {
             const sbmp_f32x2 mn = {seg_min(xy.x, nxy.x), seg_min(xy.y, nxy.y)};
             const sbmp_f32x2 mx = {seg_max(xy.x, nxy.x), seg_max(xy.y, nxy.y)};
 #pragma unroll
             for (int k = 0; k < NOBS; ++k)
-                if ((kept >> k) & 1u) sep = seg_min(sep, box_sep(mn, mx, obs[k]));   // uniform branch
+                if ((keptNow >> k) & 1u) sep = seg_min(sep, box_sep(mn, mx, obs[k]));   // uniform branch
         }
         // the reference's break: out of bounds keeps the new (x, y) and the old
-        // (theta, v); a collision keeps all four
+        // (theta, v); a collision keeps the new (x, y, theta, v) and ends the child
         const bool live = aliveF > 0.0f;
-        const float in4 = cull.bounds ? min4_asm(aliveF, nxy.x, nxy.y, __builtin_fminf(far.x, far.y)) : aliveF;
+        const float in4 = bnd ? min4_asm(aliveF, nxy.x, nxy.y, __builtin_fminf(far.x, far.y)) : aliveF;
         const bool upd = in4 > 0.0f;   // alive & inside
         xy = live ? nxy : xy;
         vt = upd ? nvt : vt;

@@ -1377,7 +1377,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) voi
     const SBMP_GAS unsigned long long* const pubCur = G(d.stepPub) + (size_t)cp * (d.nR1 + nW);
     // d.timeline if this launch is the traced one (decided on the host: no dependent
     // loads of the plan struct before the prologue's own).  Only a diagnostic build
-    // (SBMP_HIPCC_FLAGS=-DSBMP_TIMELINE, tools/_tl.sh) stamps: held in registers, the
+    // (SBMP_HIPCC_FLAGS=-DSBMP_TIMELINE, tools/mk_variant.sh tl) stamps: held in registers, the
     // eight 64-bit stamps cost every wave ~30 VALU of zeroing and moves.
 #ifdef SBMP_TIMELINE
     long long* const tl = tlBase ? tlBase + ((size_t)b * (kBlock / kWave) + wave) * kTimelineStamps : nullptr;
@@ -1415,6 +1415,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) voi
                  "s"(d.treeCtrl), "s"(d.stepList));
     float4 obsReg = make_float4(0.f, 0.f, 0.f, 0.f);
     if (kLdsObs && tid < d.nObs) obsReg = G(d.obstacles)[tid];
+    // register lists: box (lane % n) for the per-step schedule (car_schedule)
+    float4 oLane = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (AGENT == 0 && kRegObs > 0) oLane = G(d.obstacles)[lane % (kRegObs > 0 ? kRegObs : 1)];
     sR1P[tid] = 0;   // nR1 == kBlock
     for (int i = tid; i < nW; i += kBlock) sNew[i] = 0u;
     // ---- the child's controls (statePropagator.cu:17-21) depend on the slot's stream
@@ -1606,11 +1609,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) voi
         fast = car_fast_ok(d);   // per plan (uniform)
         if (fast) {
             // a huge steering tan can drive theta past Cody-Waite's range within a child
-            const WaveCull cull = car_cull<OBS>(p, ctl, d, obs);
+            const StepSched sched = car_schedule<OBS>(p, parent, act, d, oLane);
+            WaveCull cull{~0u, true};   // the schedule covers the whole reach
+            if (!sched.valid) cull = car_cull<OBS>(p, ctl, d, obs);
             if (__ballot(!car_theta_bounded(p, ctl, d)) == 0ull)
-                valid = car_euler_fast<OBS, false>(p, ctl, d, obs, cull, out) && act;
+                valid = car_euler_fast<OBS, false>(p, ctl, d, obs, cull, sched, out) && act;
             else
-                valid = car_euler_fast<OBS, true>(p, ctl, d, obs, cull, out) && act;
+                valid = car_euler_fast<OBS, true>(p, ctl, d, obs, cull, sched, out) && act;
         }
     }
     if (!fast) {
@@ -1724,11 +1729,20 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) voi
             store_record_g(e + 1, cc);
             store_record_g(e + 2, make_float4(cost, 0.0f, 0.0f, 0.0f));
         } else {
+#ifdef SBMP_SOFFSET_DEMO   // the round-3 form of these stores (kgmt_device.h, SBMP_WT_OFF)
+            const __amdgpu_buffer_rsrc_t rl = wt_rsrc(d.stepList);
+            const int so = __builtin_amdgcn_readfirstlane(((cp * d.nBlocks + b) * kBlock) * kStepEntry * 16);
+            const int vo = (waveOff + idxW) * kStepEntry * 16;
+            __builtin_amdgcn_raw_buffer_store_b128(sbmp_u32x4{__float_as_uint(cs.x), __float_as_uint(cs.y), __float_as_uint(cs.z), __float_as_uint(cs.w)}, rl, vo, so, 0);
+            __builtin_amdgcn_raw_buffer_store_b128(sbmp_u32x4{__float_as_uint(cc.x), __float_as_uint(cc.y), __float_as_uint(cc.z), __float_as_uint(cc.w)}, rl, vo + 16, so, 0);
+            __builtin_amdgcn_raw_buffer_store_b128(sbmp_u32x4{__float_as_uint(cost), 0u, 0u, 0u}, rl, vo + 32, so, 0);
+#else
             SBMP_GAS float4* e =
                 G(d.stepList) + ((size_t)cp * d.nBlocks * kBlock + (size_t)b * kBlock + waveOff + idxW) * kStepEntry;
             e[0] = cs;
             e[1] = cc;
             e[2] = make_float4(cost, 0.0f, 0.0f, 0.0f);
+#endif
         }
     }
     {   // one 64-bit atomic per touched cell, into this workgroup's replica
@@ -1990,6 +2004,51 @@ static void launch_step_form(const KgmtDev& d, int t, int expand, int variant, h
         launch(k_step<AGENT, kObsLds, SH>, grid, block, shm, s, tm, SBMP_STEP_ARGS);
     }
 #undef SBMP_STEP_ARGS
+}
+
+// The k_step instantiation launch_step_form picks, and its dynamic LDS, for the
+// residency check (step_resident_groups).
+using StepFn = void (*)(const KgmtDev*, int, int, const int4*, const IterCtrl*, const uint4*, const uint2*,
+                        const unsigned long long*, const PlannerStatus*, long long*);
+template <int AGENT, bool SH>
+static StepFn step_fn(const KgmtDev& d, int variant, size_t* shm) {
+    const size_t nS = SH ? d.nBlocks / d.nranks : d.nBlocks;
+    const size_t pfx = sizeof(int) * (nS + 1) + sizeof(uint32_t) * (size_t)(d.nR2 / 32);
+    *shm = pfx;
+    if (d.gridStart) return k_step<AGENT, kObsGrid, SH>;
+    if (d.nObs > kMaxLdsObs) return k_step<AGENT, kObsGlobal, SH>;
+    if (d.nObs <= kMaxRegObs && (variant == 0 || variant == 3)) {
+        switch (d.nObs) {
+            case 0: return k_step<AGENT, kObsReg + 0, SH>;
+            case 1: return k_step<AGENT, kObsReg + 1, SH>;
+            case 2: return k_step<AGENT, kObsReg + 2, SH>;
+            case 3: return k_step<AGENT, kObsReg + 3, SH>;
+            case 4: return k_step<AGENT, kObsReg + 4, SH>;
+            case 5: return k_step<AGENT, kObsReg + 5, SH>;
+            case 6: return k_step<AGENT, kObsReg + 6, SH>;
+            case 7: return k_step<AGENT, kObsReg + 7, SH>;
+            default: return k_step<AGENT, kObsReg + 8, SH>;
+        }
+    }
+    *shm = sizeof(float4) * (size_t)d.nObs + pfx;   // LDS obstacle forms
+    return (variant == 2) ? k_step<AGENT, kObsLds4, SH> : k_step<AGENT, kObsLds, SH>;
+}
+
+int step_resident_groups(const KgmtDev& d, int agent, int variant) {
+    size_t shm = 0;
+    StepFn fn;
+    if (agent == 0) fn = d.sharded ? step_fn<0, true>(d, variant, &shm) : step_fn<0, false>(d, variant, &shm);
+    else fn = d.sharded ? step_fn<1, true>(d, variant, &shm) : step_fn<1, false>(d, variant, &shm);
+    int dev = 0, cus = 0, perCU = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
+    if (shm > 65536)   // LDS above 64 KB needs the opt-in (not reached by k_step's forms, kept for safety)
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(fn), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)shm);
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&perCU, reinterpret_cast<const void*>(fn), kBlock, shm) !=
+        hipSuccess)
+        return 0;
+    return perCU * cus;
 }
 
 template <int AGENT>

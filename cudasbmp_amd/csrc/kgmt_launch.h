@@ -25,6 +25,10 @@ void launch_expand(const KgmtDev& d, int t, int agent, int blocks, int variant, 
 // k_step(t): one launch per iteration on a single rank; expand == 0: flush pass.
 void launch_step(const KgmtDev& d, int t, int expand, int agent, int variant, hipStream_t s,
                  const KernelTiming& tm = KernelTiming());
+// Workgroups of the k_step form launch_step would pick for d that the device holds at
+// once (occupancy per CU x CUs); k_step needs all of its 1 + blocks resident, since
+// its expanders wait for workgroup 0.  0 if the query fails.
+int step_resident_groups(const KgmtDev& d, int agent, int variant);
 void launch_fold_r2(const KgmtDev& d, int tFirst, int tLast, hipStream_t s, const KernelTiming& tm = KernelTiming());
 // k_finish(t): insert iteration t (insertBlocks = every global 256-slot block) +
 // prepare iteration t+1.  t = 0 prepares iteration 1 only (insertBlocks = 0).

@@ -160,6 +160,8 @@ KgmtPlanner::KgmtPlanner(const sbmp_kgmt_params& p, int nranks, int rank, Exchan
     d.rcpR2Size = markstein_rcp(d.R2Size);
     d.rcpNumDisc = markstein_rcp((float)p.numDisc);
     d.rcpAgentLength = markstein_rcp(p.agentLength);
+    // dt = duration / numDisc <= 1.05 / numDisc (statePropagator.cu:19-21); 1% above it
+    d.reachStep = p.numDisc > 0 ? 1.06f / (float)p.numDisc : 0.0f;
 
     d.treeState = alloc<float4>(M);
     d.treeCtrl = alloc<float4>(M);
@@ -249,17 +251,19 @@ KgmtPlanner::KgmtPlanner(const sbmp_kgmt_params& p, int nranks, int rank, Exchan
     d.sharded = nranks > 1 || ex != nullptr;   // one RCCL rank still takes the sharded path
     // One launch per iteration (k_step) on a single rank whose block prefix fits LDS;
     // SBMP_STEP=0 keeps the two-kernel form (k_expand + k_finish).
-    d.stepMode = 0;
+    // begin() confirms it per plan: all 1 + blocks workgroups must be resident at once
+    // for the obstacle form the plan's list picks (step_resident_groups).
     {
         const char* v = getenv("SBMP_STEP");
-        if ((!d.sharded && d.nBlocks <= kMaxStepBlocks && !(v && atoi(v) == 0)) || shStep_) d.stepMode = 1;
+        stepCapable_ = (!d.sharded && d.nBlocks <= kMaxStepBlocks && !(v && atoi(v) == 0)) || shStep_;
     }
+    d.stepMode = stepCapable_ ? 1 : 0;
     d.stepCnt = nullptr;
     d.stepPub = nullptr;
     d.stepList = nullptr;
     d.stepDelta = nullptr;
     d.stepR2New = nullptr;
-    if (d.stepMode) {
+    if (stepCapable_) {
         d.stepPub = alloc<unsigned long long>((size_t)2 * (d.nR1 + d.nR2 / 32));
         if (!d.sharded) {   // a sharded rank's counts, deltas and R2New travel in the exchange, its lists in recOut
             d.stepCnt = alloc<int>((size_t)2 * kMaxStepBlocks);
@@ -418,8 +422,8 @@ void KgmtPlanner::begin(const float* initial, const float* goal, const float* d_
     if (xRecv_ != xSend_) SBMP_HIP(hipMemsetAsync(xRecv_, 0, sizeof(unsigned long long) * xWords_, s));
     SBMP_HIP(hipMemsetAsync(d.R1, 0, sizeof(int) * 2 * 5 * d.nR1, s));   // both parities
     SBMP_HIP(hipMemsetAsync(d.R2Avail, 0, sizeof(uint32_t) * 2 * (d.nR2 / 32), s));
-    if (d.stepMode) SBMP_HIP(hipMemsetAsync(d.stepPub, 0, sizeof(unsigned long long) * 2 * (d.nR1 + d.nR2 / 32), s));
-    if (d.stepMode && !d.sharded) {
+    if (stepCapable_) SBMP_HIP(hipMemsetAsync(d.stepPub, 0, sizeof(unsigned long long) * 2 * (d.nR1 + d.nR2 / 32), s));
+    if (stepCapable_ && !d.sharded) {
         SBMP_HIP(hipMemsetAsync(d.stepCnt, 0, sizeof(int) * 2 * kMaxStepBlocks, s));
         SBMP_HIP(hipMemsetAsync(d.stepDelta, 0, sizeof(unsigned long long) * 3 * kDeltaReps * d.nR1, s));
         SBMP_HIP(hipMemsetAsync(d.stepR2New, 0, sizeof(uint32_t) * 3 * kNewReps * (d.nR2 / 32), s));
@@ -457,7 +461,81 @@ void KgmtPlanner::begin(const float* initial, const float* goal, const float* d_
     d.gridInvW = d.gridInvH = 0.0f;
     d.gridStart = nullptr;
     d.gridBoxes = nullptr;
-    if (nObs > 0 && ((nObs > kMaxLdsObs && expandVariant_ != 5) || expandVariant_ == 4)) {
+    if (nObs > 0 && ((nObs > kMaxLdsObs && expandVariant_ != 5) || expandVariant_ == 4)) build_grid(d_obstacles, nObs);
+    choose_form(d_obstacles, nObs);
+    d.goalX = goal[0];
+    d.goalY = goal[1];
+
+    // Root (KGMT.cu:85-97).
+    const int r1 = getR1(initial[0], initial[1], d.R1Size, d.N);
+    const int r2 = getR2(initial[0], initial[1], r1, d.R1Size, d.N, d.R2Size, d.n);
+    launch_seed_root(d, make_float4(initial[0], initial[1], initial[2], initial[3]),
+                     make_float4(initial[4], initial[5], initial[6], 0.0f), r1, r2, s);
+    // curand_init(seed, slot, 0) for every slot (KGMT.cu:109-111, D1).
+    launch_init_slots(d, curand_seed_state(seed), jumps_, nbits_, expandBlocks_, s);
+    SBMP_HIP(hipGetLastError());
+
+    t_next_ = 1;
+    lastFolded_ = 0;
+    begun_ = true;
+    wallMs_ = 0.0;
+    SBMP_HIP(hipStreamSynchronize(s));
+    if (ex_) ex_->barrier(s);   // every rank set up before the first (time-bounded) exchange
+    t0_ = now_ms();
+    if (d.stepMode) flushed_ = false;   // k_step(1) plans iteration 1 itself
+    else launch_finish(d, 0, 0, s, timing(K_FINISH));   // prepares iteration 1
+    SBMP_HIP(hipGetLastError());
+}
+
+void KgmtPlanner::choose_form(const float* d_obstacles, int nObs) {
+    KgmtDev& d = d_;
+    // k_step's expanders wait for workgroup 0, so every workgroup of the launch must be
+    // resident at once; the dispatch order is not defined.  A list that leaves too few
+    // workgroups per CU (LDS near kMaxLdsObs boxes at 262,144 slots per rank) takes the
+    // two-launch form on one rank, and the grid index on a sharded rank (whose exchange
+    // layout is k_step's); both are bit-exact for every list.
+    d.stepMode = stepCapable_ ? 1 : 0;
+    neededGroups_ = 1 + (d.sharded ? d.nBlocks / d.nranks : d.nBlocks);
+    residentGroups_ = stepCapable_ ? step_resident_groups(d, p_.agent, expandVariant_) : 0;
+    if (stepCapable_ && residentGroups_ < neededGroups_) {
+        const int before = residentGroups_;
+        if (!d.sharded) {
+            d.stepMode = 0;
+        } else if (!d.gridStart && nObs > 0) {
+            build_grid(d_obstacles, nObs);
+            residentGroups_ = step_resident_groups(d, p_.agent, expandVariant_);
+        }
+        if (d.sharded && residentGroups_ < neededGroups_)
+            throw Error(SBMP_ERR_INVALID_ARGUMENT, "k_step needs " + std::to_string(neededGroups_) +
+                                                       " resident workgroups per rank; the device holds " +
+                                                       std::to_string(residentGroups_));
+        if (!formLogged_) {
+            fprintf(stderr, "sbmp: %d obstacles: k_step needs %d workgroups resident, the device holds %d; %s\n", nObs,
+                    neededGroups_, before,
+                    d.sharded ? "this rank indexes the obstacles with the uniform grid" : "two launches per iteration");
+            formLogged_ = true;
+        }
+    }
+}
+
+void KgmtPlanner::path_info(sbmp_path_info* out) {
+    const KgmtDev& d = d_;
+    out->stepForm = d.stepMode ? 1 : 0;
+    out->obstacleForm = d.gridStart                    ? SBMP_OBS_GRID
+                        : d.nObs > kMaxLdsObs           ? SBMP_OBS_GLOBAL
+                        : (d.nObs <= kMaxRegObs && (expandVariant_ == 0 || expandVariant_ == 3)) ? SBMP_OBS_REGISTERS
+                                                        : SBMP_OBS_LDS;
+    out->residentGroups = residentGroups_;
+    out->neededGroups = neededGroups_;
+    out->exchange = !d.sharded ? SBMP_EXCHANGE_NONE : (oneshot_ ? SBMP_EXCHANGE_ONESHOT : SBMP_EXCHANGE_COLLECTIVE);
+    out->nranks = d.nranks;
+    out->rank = d.rank;
+    out->commRanks = ex_ ? ex_->comm_ranks() : 0;
+}
+
+void KgmtPlanner::build_grid(const float* d_obstacles, int nObs) {
+    KgmtDev& d = d_;
+    {
         std::vector<float> h((size_t)4 * nObs);
         SBMP_HIP(hipMemcpy(h.data(), d_obstacles, sizeof(float) * h.size(), hipMemcpyDeviceToHost));
         const HostObstacleGrid g = build_obstacle_grid(h.data(), nObs, d.width, d.height, 0);
@@ -483,28 +561,6 @@ void KgmtPlanner::begin(const float* initial, const float* goal, const float* d_
         d.gridStart = gridStart_;
         d.gridBoxes = gridBoxes_;
     }
-    d.goalX = goal[0];
-    d.goalY = goal[1];
-
-    // Root (KGMT.cu:85-97).
-    const int r1 = getR1(initial[0], initial[1], d.R1Size, d.N);
-    const int r2 = getR2(initial[0], initial[1], r1, d.R1Size, d.N, d.R2Size, d.n);
-    launch_seed_root(d, make_float4(initial[0], initial[1], initial[2], initial[3]),
-                     make_float4(initial[4], initial[5], initial[6], 0.0f), r1, r2, s);
-    // curand_init(seed, slot, 0) for every slot (KGMT.cu:109-111, D1).
-    launch_init_slots(d, curand_seed_state(seed), jumps_, nbits_, expandBlocks_, s);
-    SBMP_HIP(hipGetLastError());
-
-    t_next_ = 1;
-    lastFolded_ = 0;
-    begun_ = true;
-    wallMs_ = 0.0;
-    SBMP_HIP(hipStreamSynchronize(s));
-    if (ex_) ex_->barrier(s);   // every rank set up before the first (time-bounded) exchange
-    t0_ = now_ms();
-    if (d.stepMode) flushed_ = false;   // k_step(1) plans iteration 1 itself
-    else launch_finish(d, 0, 0, s, timing(K_FINISH));   // prepares iteration 1
-    SBMP_HIP(hipGetLastError());
 }
 
 void KgmtPlanner::enqueue(int iterations) {

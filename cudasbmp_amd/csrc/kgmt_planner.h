@@ -39,6 +39,7 @@ public:
     // one-shot exchange waits for its peers in-kernel with a time bound, so ranks are
     // lined up here before their first exchange and after host-side pauses (dumps).
     virtual void barrier(hipStream_t s) = 0;
+    virtual int comm_ranks() const { return 0; }   // ranks of the RCCL communicator, 0 if none
 };
 
 // What the C ABI drives: one rank (single GPU or one rank of an RCCL group) or a
@@ -78,6 +79,7 @@ public:
     void export_csv(const std::string& dir);
 
     virtual std::vector<sbmp_kernel_stat> kernel_stats() = 0;
+    virtual void path_info(sbmp_path_info* out) = 0;
     virtual void reset_kernel_stats() = 0;
     virtual void set_profiling(bool on) = 0;
     virtual void enqueue_delay(double us) = 0;
@@ -129,6 +131,7 @@ public:
     int solution_path(int node, int* rows, float* samples, float* costs, int capacity) override;
 
     std::vector<sbmp_kernel_stat> kernel_stats() override;
+    void path_info(sbmp_path_info* out) override;
     void reset_kernel_stats() override;
     void set_profiling(bool on) override { p_.profileKernels = on ? 1 : 0; }
     void enqueue_delay(double us) override { launch_delay(us, stream_); }
@@ -192,6 +195,11 @@ private:
     unsigned long long* xSend_ = nullptr;
     unsigned long long* xSendOdd_ = nullptr;   // sharded k_step: the send buffer of odd iterations
     bool shStep_ = false;                      // sharded rank in k_step mode
+    bool stepCapable_ = false;                 // k_step buffers exist; begin() decides per plan (d_.stepMode)
+    int residentGroups_ = 0, neededGroups_ = 0;   // k_step residency at the last begin()
+    bool formLogged_ = false;
+    void choose_form(const float* d_obstacles, int nObs);
+    void build_grid(const float* d_obstacles, int nObs);
     unsigned long long* xRecv_ = nullptr;
     size_t xWords_ = 0;
     bool oneshot_ = false;                   // sharded: the exchange is k_oneshot over IPC-mapped inboxes
@@ -260,6 +268,7 @@ public:
     }
 
     std::vector<sbmp_kernel_stat> kernel_stats() override { return r0().kernel_stats(); }
+    void path_info(sbmp_path_info* out) override { r0().path_info(out); }
     void reset_kernel_stats() override;
     void set_profiling(bool on) override;
     void enqueue_delay(double us) override { r0().enqueue_delay(us); }

@@ -48,6 +48,10 @@ public:
         if (setup_) (void)hipStreamDestroy(setup_);
         if (comm_) (void)ncclCommDestroy(comm_);
     }
+    int comm_ranks() const override {
+        int n = 0;
+        return (comm_ && ncclCommCount(comm_, &n) == ncclSuccess) ? n : 0;
+    }
 
     void allreduce_u64(const unsigned long long* send, unsigned long long* recv, size_t n, hipStream_t s) override {
         SBMP_NCCL(ncclAllReduce(send, recv, n, ncclUint64, ncclSum, comm_, s));

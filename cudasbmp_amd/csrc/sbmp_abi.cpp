@@ -368,6 +368,14 @@ sbmp_status sbmp_kgmt_kernel_stats(sbmp_kgmt* h, sbmp_kernel_stat* out, int capa
     });
 }
 
+sbmp_status sbmp_kgmt_path_info(sbmp_kgmt* h, sbmp_path_info* out) {
+    return guarded([&] {
+        PLANNER(h);
+        REQUIRE(out, "out must be non-NULL");
+        P.path_info(out);
+    });
+}
+
 sbmp_status sbmp_kgmt_reset_kernel_stats(sbmp_kgmt* h) {
     return guarded([&] {
         PLANNER(h);

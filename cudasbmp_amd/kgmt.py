@@ -321,6 +321,19 @@ class KGMT:
     def reset_kernel_stats(self) -> None:
         nat.call("sbmp_kgmt_reset_kernel_stats", self._h)
 
+    OBSTACLE_FORMS = ("registers", "lds", "grid", "global")
+    EXCHANGES = ("none", "oneshot", "collective")
+
+    def path_info(self) -> dict:
+        """The form of the hot path chosen at the last begin() (sbmp_kgmt_path_info)."""
+        pi = nat.PathInfo()
+        nat.call("sbmp_kgmt_path_info", self._h, ctypes.byref(pi))
+        return {"form": "k_step" if pi.stepForm else "two-launch",
+                "obstacle_form": self.OBSTACLE_FORMS[pi.obstacleForm] if 0 <= pi.obstacleForm < 4 else pi.obstacleForm,
+                "resident_groups": pi.residentGroups, "needed_groups": pi.neededGroups,
+                "exchange": self.EXCHANGES[pi.exchange] if 0 <= pi.exchange < 3 else pi.exchange,
+                "nranks": pi.nranks, "rank": pi.rank, "rccl_nranks": pi.commRanks}
+
     def kernel_samples(self, name: str) -> np.ndarray:
         """Per-launch durations (ms) of kernel `name` since the last reset_kernel_stats()."""
         cnt = ctypes.c_int()

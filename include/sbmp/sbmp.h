@@ -95,6 +95,25 @@ typedef struct sbmp_kernel_stat {
     double totalMs;           /* sum of HIP-event durations on the planner's stream */
 } sbmp_kernel_stat;
 
+/* Which form of the hot path a planner runs (sbmp_kgmt_path_info): no reference
+ * counterpart (the reference has one form, KGMT.cu:118-292); for logs and bench lines. */
+#define SBMP_OBS_REGISTERS 0  /* <= 8 boxes held in registers (wave cull + per-step schedule) */
+#define SBMP_OBS_LDS 1        /* <= 2,048 boxes staged in LDS per workgroup */
+#define SBMP_OBS_GRID 2       /* uniform-grid obstacle index (include/sbmp/obstacle_grid.h) */
+#define SBMP_OBS_GLOBAL 3     /* the all-boxes loop from global memory (diagnostics) */
+#define SBMP_EXCHANGE_NONE 0      /* one rank */
+#define SBMP_EXCHANGE_ONESHOT 1   /* k_oneshot through IPC-mapped inboxes (sharded default) */
+#define SBMP_EXCHANGE_COLLECTIVE 2 /* the communicator's all-reduce (RCCL, or host callbacks) */
+typedef struct sbmp_path_info {
+    int stepForm;             /* 1: one k_step launch per iteration; 0: k_expand + k_finish (+ k_pack) */
+    int obstacleForm;         /* SBMP_OBS_* of the last begin() */
+    int residentGroups;       /* k_step workgroups the device holds at once (occupancy x CUs), 0 if not k_step-capable */
+    int neededGroups;         /* 1 + blocks per rank: k_step needs them all resident */
+    int exchange;             /* SBMP_EXCHANGE_* */
+    int nranks, rank;
+    int commRanks;            /* ranks of the RCCL communicator (0: none) */
+} sbmp_path_info;
+
 typedef struct sbmp_kgmt sbmp_kgmt;
 
 int sbmp_abi_version(void);
@@ -185,6 +204,8 @@ sbmp_status sbmp_kgmt_solution_path(sbmp_kgmt* h, int node, int* rows, float* sa
                                     int* length);
 
 sbmp_status sbmp_kgmt_kernel_stats(sbmp_kgmt* h, sbmp_kernel_stat* out, int capacity, int* count);
+/* The form of the hot path chosen at the last begin() (sbmp_path_info). */
+sbmp_status sbmp_kgmt_path_info(sbmp_kgmt* h, sbmp_path_info* out);
 sbmp_status sbmp_kgmt_reset_kernel_stats(sbmp_kgmt* h);
 /* Turn per-launch HIP-event timing on/off for subsequently enqueued iterations. */
 sbmp_status sbmp_kgmt_set_profiling(sbmp_kgmt* h, int enabled);

@@ -111,3 +111,44 @@ def test_c5_1M_bit_exact(oracle_lib):
     g, o, r = _run(_bench_kw(1 << 20, 3), BENCH_SEED, obs)
     assert g.iter_log()[:, 5].max() == 1 << 20
     assert_same_state(g, o, label="c5 1M")
+
+
+def test_c3_lds_2048_boxes_takes_the_two_launch_form(oracle_lib):
+    """k_step needs all 1 + 1,024 workgroups resident (its expanders wait for workgroup
+    0); a 2,048-box LDS list (32 KB per workgroup) leaves 4 per CU, 1,024 on the chip,
+    so begin() picks the two-launch form (KGMT.cu:151-249 as k_expand + k_finish).
+    Bit-exact against the oracle at c3 size."""
+    obs = _c5_obstacles()[:2048].copy()
+    g, o, r = _run(_bench_kw(262144, 3), BENCH_SEED, obs)
+    info = g.path_info()
+    assert info["obstacle_form"] == "lds" and info["form"] == "two-launch", info
+    assert 0 < info["resident_groups"] < info["needed_groups"] == 1025, info
+    assert g.iter_log()[:, 5].max() == 262144
+    assert_same_state(g, o, label="c3 2,048-box LDS list")
+
+
+def test_sharded_lds_2048_boxes_takes_the_grid(oracle_lib):
+    """A sharded rank keeps k_step (its exchange layout), so when the LDS list does not
+    leave room for all its workgroups it indexes the boxes with the uniform grid: 2 ranks
+    of 1,024 blocks each (524,288 children), bit-exact."""
+    obs = _c5_obstacles()[:2048].copy()
+    g, o, r = _run(_bench_kw(1 << 19, 2, maxTreeSize=1 << 25), BENCH_SEED, obs, P=2)
+    info = g.path_info()
+    assert info["form"] == "k_step" and info["obstacle_form"] == "grid", info
+    assert info["needed_groups"] == 1025 and info["resident_groups"] >= 1025, info
+    assert_same_state(g, o, label="2 ranks, 2,048-box list on the grid")
+
+
+def test_c3_path_info_is_k_step():
+    from cudasbmp_amd import KGMT, DeviceBuffer
+    from conftest import OBSTACLES_CSV
+    obs = np.loadtxt(OBSTACLES_CSV, delimiter=",", dtype=np.float32).reshape(-1, 4)
+    cfg = dict(DEMO)
+    kw = _bench_kw(262144, 2)
+    extra = {k: kw.pop(k) for k in ("samplesPerIteration", "fixGNewClear", "batchRule")}
+    cfg.update(kw)
+    g = KGMT(**cfg, **extra)
+    g.plan(DEMO_INITIAL, DEMO_GOAL, DeviceBuffer(obs), len(obs), seed=BENCH_SEED)
+    info = g.path_info()
+    assert info["form"] == "k_step" and info["obstacle_form"] == "registers" and info["exchange"] == "none", info
+    assert info["resident_groups"] >= info["needed_groups"] == 1025, info
