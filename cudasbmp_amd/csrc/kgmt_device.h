@@ -185,7 +185,7 @@ struct KgmtDev {
     long long* timeline;
     long long* timelineFin;   // k_finish(timelineIter): [1 + nBlocks][kTimelineStamps], wave 0 of each workgroup
     int timelineIter;
-    int obsNaN;   // a register-held obstacle has a NaN coordinate: wave_cull keeps every box
+    int obsNaN;   // an obstacle has a NaN coordinate: wave_cull keeps every box, the grid tests by compares
     // Sharded k_step: per-iteration exchange [R1 delta replicas | row
     // words | block words | R2New bytes].  Row b is block b of every rank (global
     // blocks b P .. b P + P - 1); every rank adds its block's count | goal flag << 16
@@ -581,6 +581,67 @@ __device__ __forceinline__ bool motion_valid_culled(float minx, float miny, floa
     return !hit;
 }
 
+// grid_motion_valid_batched (include/sbmp/obstacle_grid.h) for the kernels: the same
+// boolean from the same listed boxes, in fewer and cheaper instructions.
+//   - The CSR arrays through global-address-space pointers: loaded from the plan struct
+//     the pointers are generic, and flat loads count against lgkmcnt, so every box
+//     batch waited with vmcnt(0) lgkmcnt(0) behind the scalar and LDS traffic as well.
+//   - isBroadPhaseValid (collisionCheck.cu:6-14) as wave_cull's separation metric,
+//     max(o.xmin - maxx, minx - o.xmax, o.ymin - maxy, miny - o.ymax) < 0 iff the boxes
+//     overlap (exact for finite segments, D15, and any box without NaN; begin() sends a
+//     list with a NaN coordinate to the reference form), folded with min: VALU only,
+//     where the four compares and their mask ANDs / ORs ran on the SALU and the
+//     short-circuit OR had become branches.
+//   - A batch loads kGridBatch consecutive rows unconditionally (the box array holds
+//     kGridBatch padding rows past its end) at immediate offsets from one address, and
+//     masks the rows past the cell run, instead of clamping each index.
+//   - Cells by fmed3 (segments are finite: grid_cell's NaN case cannot arise).
+constexpr int kGridBatch = 8;   // boxes loaded per round trip; also the padding rows of gridBoxes
+
+// keep ? v : +inf as one v_cndmask on a lane mask: written as a C select, the compiler
+// sank each padded box's loads and tests into a branch of its own.
+__device__ __forceinline__ float keep_or_inf(bool keep, float v) {
+    const unsigned long long m = __ballot(keep);
+    float r;
+    asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "v"(__builtin_inff()), "v"(v), "s"(m));
+    return r;
+}
+__device__ __forceinline__ bool grid_free_fast(float minx, float miny, float maxx, float maxy, const KgmtDev& d) {
+    const SBMP_GAS int* const start = G(d.gridStart);
+    const SBMP_GAS float4* const boxes = G(d.gridBoxes);
+    const int g = d.gridG;
+    const float top = (float)(g - 1);
+    auto cell = [&](float v, float inv) { return (int)__builtin_amdgcn_fmed3f(__builtin_floorf(v * inv), 0.0f, top); };
+    const int cx0 = cell(minx, d.gridInvW), cx1 = cell(maxx, d.gridInvW);
+    const int cy0 = cell(miny, d.gridInvH), cy1 = cell(maxy, d.gridInvH);
+    const sbmp_f32x2 mn = {minx, miny}, mx = {maxx, maxy};
+    float sep = 1.0f;   // min over the tested boxes; < 0: one overlaps
+    for (int cy = cy0; cy <= cy1 && !(sep < 0.0f); cy += 2) {
+        // two cell rows' runs at once (a step's segment spans one or two rows almost always)
+        const int c1 = min(cy + 1, cy1);
+        const int b0 = start[cy * g + cx0], e0 = start[cy * g + cx1 + 1];
+        const int b1 = start[c1 * g + cx0], e1 = (cy + 1 <= cy1) ? start[c1 * g + cx1 + 1] : b1;
+#pragma unroll
+        for (int r = 0; r < 2; ++r) {
+            const int b = r ? b1 : b0, e = r ? e1 : e0;
+            for (int i = b; i < e && !(sep < 0.0f); i += kGridBatch) {
+                const SBMP_GAS float4* const row = boxes + i;
+                float4 o[kGridBatch];
+#pragma unroll
+                for (int k = 0; k < kGridBatch; ++k) o[k] = row[k];
+#pragma unroll
+                for (int k = 0; k < kGridBatch; ++k) {
+                    const sbmp_f32x2 lo = sbmp_f32x2{o[k].x, o[k].y} - mx;
+                    const sbmp_f32x2 hi = mn - sbmp_f32x2{o[k].z, o[k].w};
+                    const float s = __builtin_fmaxf(vmax3(lo.x, lo.y, hi.x), hi.y);
+                    sep = seg_min(sep, keep_or_inf(i + k < e, s));   // rows past the run test nothing
+                }
+            }
+        }
+    }
+    return !(sep < 0.0f);
+}
+
 // reference statePropagator.cu:5-76 (car).  Same operation sequence as the oracle
 // (D9-D11): fmaf where nvcc would contract, steering via one double fma.
 // v / agentLength: when agentLength is a power of two, v * (1/agentLength) is the
@@ -673,8 +734,9 @@ __device__ __forceinline__ bool car_euler(float4 p, const ChildCtl& ctl, const K
         bool freeSeg;
         if (OBS >= kObsReg) freeSeg = motion_valid_culled<OBS>(minx, miny, maxx, maxy, obs, cull.boxes);
         else if (OBS == kObsGrid)   // only lanes whose result counts walk their cells
-            freeSeg = oob || grid_motion_valid_batched(minx, miny, maxx, maxy, d.gridG, d.gridInvW, d.gridInvH,
-                                               d.gridStart, d.gridBoxes);
+            freeSeg = oob || (d.obsNaN ? grid_motion_valid_batched(minx, miny, maxx, maxy, d.gridG, d.gridInvW,
+                                                                   d.gridInvH, d.gridStart, d.gridBoxes)
+                                       : grid_free_fast(minx, miny, maxx, maxy, d));
         else freeSeg = motion_valid<OBS>(minx, miny, maxx, maxy, obs, d.nObs);
         xy = nxy;
         if (!oob) tv = ntv;
@@ -718,8 +780,9 @@ __device__ __forceinline__ bool point_euler(float4 p, const ChildCtl& ctl, const
         bool freeSeg;
         if (OBS >= kObsReg) freeSeg = motion_valid_culled<OBS>(minx, miny, maxx, maxy, obs, cull.boxes);
         else if (OBS == kObsGrid)
-            freeSeg = oob || grid_motion_valid_batched(minx, miny, maxx, maxy, d.gridG, d.gridInvW, d.gridInvH,
-                                               d.gridStart, d.gridBoxes);
+            freeSeg = oob || (d.obsNaN ? grid_motion_valid_batched(minx, miny, maxx, maxy, d.gridG, d.gridInvW,
+                                                                   d.gridInvH, d.gridStart, d.gridBoxes)
+                                       : grid_free_fast(minx, miny, maxx, maxy, d));
         else freeSeg = motion_valid<OBS>(minx, miny, maxx, maxy, obs, d.nObs);
         x = nx;
         y = ny;

@@ -539,7 +539,8 @@ void KgmtPlanner::build_grid(const float* d_obstacles, int nObs) {
         std::vector<float> h((size_t)4 * nObs);
         SBMP_HIP(hipMemcpy(h.data(), d_obstacles, sizeof(float) * h.size(), hipMemcpyDeviceToHost));
         const HostObstacleGrid g = build_obstacle_grid(h.data(), nObs, d.width, d.height, 0);
-        const size_t nStart = g.start.size(), nBoxes = std::max<size_t>(1, g.boxes.size());
+        // kGridBatch zeroed rows past the end: grid_free_fast loads whole batches
+        const size_t nStart = g.start.size(), nBoxes = g.boxes.size() + kGridBatch;
         if (nStart > gridStartCap_) {
             if (gridStart_) SBMP_HIP(hipFree(gridStart_));
             gridStart_ = nullptr;
@@ -553,8 +554,11 @@ void KgmtPlanner::build_grid(const float* d_obstacles, int nObs) {
             gridBoxesCap_ = nBoxes;
         }
         SBMP_HIP(hipMemcpy(gridStart_, g.start.data(), sizeof(int) * nStart, hipMemcpyHostToDevice));
+        SBMP_HIP(hipMemset(gridBoxes_, 0, sizeof(float4) * nBoxes));
         if (!g.boxes.empty())
             SBMP_HIP(hipMemcpy(gridBoxes_, g.boxes.data(), sizeof(float4) * g.boxes.size(), hipMemcpyHostToDevice));
+        for (float v : h)   // grid_free_fast's separation metric needs boxes without NaN
+            if (std::isnan(v)) d.obsNaN = 1;
         d.gridG = g.g;
         d.gridInvW = g.invW;
         d.gridInvH = g.invH;

@@ -46,7 +46,8 @@ def main():
                     help="children per k_expand / k_step launch in the profiled run (for bytes/child)")
     a = ap.parse_args()
     summary = {}
-    for sub in ("sq", "sq2", "fetch", "write"):
+    subs = [x for x in ("sq", "sq2", "fetch", "write") if os.path.isdir(os.path.join(a.dir, x))] or [""]
+    for sub in subs:   # the passes of tools/profile_pmc.sh, or one pass's directory
         for kern, ctrs in load(os.path.join(a.dir, sub)).items():
             short = kern.split("(")[0].replace("void ", "").replace("sbmp::", "")
             for c, vals in ctrs.items():
