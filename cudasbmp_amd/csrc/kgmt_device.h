@@ -606,24 +606,50 @@ __device__ __forceinline__ float keep_or_inf(bool keep, float v) {
     asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "v"(__builtin_inff()), "v"(v), "s"(m));
     return r;
 }
-__device__ __forceinline__ bool grid_free_fast(float minx, float miny, float maxx, float maxy, const KgmtDev& d) {
+// The segment's cell span and the start offsets of its first two cell rows (grid_run_sep
+// tests their boxes).
+struct GridRun {
+    int cx0, cx1, cy0, cy1;
+    int b0, e0, b1, e1;   // runs of rows cy0 and cy0 + 1 (e1 = b1 for a one-row span)
+};
+
+__device__ __forceinline__ GridRun grid_run(float minx, float miny, float maxx, float maxy, const KgmtDev& d) {
     const SBMP_GAS int* const start = G(d.gridStart);
-    const SBMP_GAS float4* const boxes = G(d.gridBoxes);
     const int g = d.gridG;
     const float top = (float)(g - 1);
     auto cell = [&](float v, float inv) { return (int)__builtin_amdgcn_fmed3f(__builtin_floorf(v * inv), 0.0f, top); };
-    const int cx0 = cell(minx, d.gridInvW), cx1 = cell(maxx, d.gridInvW);
-    const int cy0 = cell(miny, d.gridInvH), cy1 = cell(maxy, d.gridInvH);
+    GridRun q;
+    q.cx0 = cell(minx, d.gridInvW);
+    q.cx1 = cell(maxx, d.gridInvW);
+    q.cy0 = cell(miny, d.gridInvH);
+    q.cy1 = cell(maxy, d.gridInvH);
+    const int c1 = min(q.cy0 + 1, q.cy1);
+    q.b0 = start[q.cy0 * g + q.cx0];
+    q.e0 = start[q.cy0 * g + q.cx1 + 1];
+    q.b1 = start[c1 * g + q.cx0];
+    q.e1 = (q.cy0 + 1 <= q.cy1) ? start[c1 * g + q.cx1 + 1] : q.b1;
+    return q;
+}
+
+// min over the span's boxes of the separation metric (< 0: a box overlaps the segment box).
+__device__ __forceinline__ float grid_run_sep(GridRun q, float minx, float miny, float maxx, float maxy,
+                                              const KgmtDev& d) {
+    const SBMP_GAS int* const start = G(d.gridStart);
+    const SBMP_GAS float4* const boxes = G(d.gridBoxes);
+    const int g = d.gridG;
     const sbmp_f32x2 mn = {minx, miny}, mx = {maxx, maxy};
-    float sep = 1.0f;   // min over the tested boxes; < 0: one overlaps
-    for (int cy = cy0; cy <= cy1 && !(sep < 0.0f); cy += 2) {
-        // two cell rows' runs at once (a step's segment spans one or two rows almost always)
-        const int c1 = min(cy + 1, cy1);
-        const int b0 = start[cy * g + cx0], e0 = start[cy * g + cx1 + 1];
-        const int b1 = start[c1 * g + cx0], e1 = (cy + 1 <= cy1) ? start[c1 * g + cx1 + 1] : b1;
+    float sep = 1.0f;
+    for (int cy = q.cy0; cy <= q.cy1 && !(sep < 0.0f); cy += 2) {
+        if (cy > q.cy0) {   // a span of three or more rows: the next two rows' runs
+            const int c1 = min(cy + 1, q.cy1);
+            q.b0 = start[cy * g + q.cx0];
+            q.e0 = start[cy * g + q.cx1 + 1];
+            q.b1 = start[c1 * g + q.cx0];
+            q.e1 = (cy + 1 <= q.cy1) ? start[c1 * g + q.cx1 + 1] : q.b1;
+        }
 #pragma unroll
         for (int r = 0; r < 2; ++r) {
-            const int b = r ? b1 : b0, e = r ? e1 : e0;
+            const int b = r ? q.b1 : q.b0, e = r ? q.e1 : q.e0;
             for (int i = b; i < e && !(sep < 0.0f); i += kGridBatch) {
                 const SBMP_GAS float4* const row = boxes + i;
                 float4 o[kGridBatch];
@@ -633,13 +659,17 @@ __device__ __forceinline__ bool grid_free_fast(float minx, float miny, float max
                 for (int k = 0; k < kGridBatch; ++k) {
                     const sbmp_f32x2 lo = sbmp_f32x2{o[k].x, o[k].y} - mx;
                     const sbmp_f32x2 hi = mn - sbmp_f32x2{o[k].z, o[k].w};
-                    const float s = __builtin_fmaxf(vmax3(lo.x, lo.y, hi.x), hi.y);
-                    sep = seg_min(sep, keep_or_inf(i + k < e, s));   // rows past the run test nothing
+                    const float sk = __builtin_fmaxf(vmax3(lo.x, lo.y, hi.x), hi.y);
+                    sep = seg_min(sep, keep_or_inf(i + k < e, sk));   // rows past the run test nothing
                 }
             }
         }
     }
-    return !(sep < 0.0f);
+    return sep;
+}
+
+__device__ __forceinline__ bool grid_free_fast(float minx, float miny, float maxx, float maxy, const KgmtDev& d) {
+    return !(grid_run_sep(grid_run(minx, miny, maxx, maxy, d), minx, miny, maxx, maxy, d) < 0.0f);
 }
 
 // reference statePropagator.cu:5-76 (car).  Same operation sequence as the oracle

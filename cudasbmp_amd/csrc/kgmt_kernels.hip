@@ -1368,16 +1368,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) voi
     const int tid = threadIdx.x;
     const int lane = tid & (kWave - 1);
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // uniform
-#ifdef SBMP_AGE_PRIO
-    {   // workgroups i, i + 256, i + 512, i + 768 share a CU (round-robin dispatch), one wave of
-        // each per SIMD, and the arbiter issues the oldest wave first: the last one dispatched
-        // finished alone at half rate.  Younger waves get a higher priority to even them out.
-        const int age = (int)blockIdx.x >> 8;
-        if (age == 1) __builtin_amdgcn_s_setprio(1);
-        else if (age == 2) __builtin_amdgcn_s_setprio(2);
-        else if (age >= 3) __builtin_amdgcn_s_setprio(3);
-    }
-#endif
     __shared__ int2 sWaveDiv[kBlock / kWave];   // (frontier position, remainder) of each wave's first slot
     const int b = (int)blockIdx.x - 1;                // this workgroup's 256-slot block (owned index)
     const int gb = SH ? d.rank + d.nranks * b : b;   // global block
