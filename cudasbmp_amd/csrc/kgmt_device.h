@@ -196,6 +196,12 @@ struct KgmtDev {
     // block, read by every rank with system-scope loads.
     unsigned long long* stepXs[2];
     const unsigned long long* stepXr;
+    // [2][nBlocks][kBlock][kStepEntry]: every rank's lists of the last iteration, pushed
+    // here by every rank's k_step (null with the collective exchange or in a local group:
+    // the lists are read from the owners' record buffers)
+    float4* stepMirror;
+    float4* mirrorPeer[kMaxRanks];   // every rank's stepMirror, mapped here
+    int listPlain;   // sharded lists readable with plain loads (the mirror, or a local shard group)
     int xRowOff, xCntOff, xNewOff;   // u64 offsets of the row words, block words and R2New bytes
     // k_step reads this struct from device memory (a copy the host refreshes before a
     // launch when it changed): as a 600-B kernel argument its fields were loaded at

@@ -792,54 +792,165 @@ __global__ __launch_bounds__(kBlock) void k_finish(KgmtDev d, int t) {
 // RCCL all-reduce of the exchange buffer.  Every rank's inbox is
 // [2 parities][nranks slots][n words] followed by flags[nranks][kOneshotChunks].
 // Workgroup c owns chunk c of the words: it stores the chunk into slot `rank` of every
-// rank's inbox (parity seq & 1) with system-scope stores, fences, raises its flag
-// (seq) at every rank, waits for every rank's flag of chunk c in its own inbox, and
-// sums the chunk's slots.  seq counts the exchanges of the plan's lifetime and is the
-// same on every rank; a rank is at most one exchange ahead of another (it waits for
+// peer's inbox (parity seq & 1) with system-scope stores, fences, raises its flag
+// (seq) at every peer, waits for every peer's flag of chunk c in its own inbox, and
+// combines the chunk's slots with its own words (read again from send, not stored).  seq counts the exchanges of the plan's lifetime and is
+// the same on every rank; a rank is at most one exchange ahead of another (it waits for
 // the other's flags), so it writes parity seq & 1 only after every reader of exchange
-// seq - 2 has summed it.
-constexpr int kOneshotChunks = 8;
+// seq - 2 has combined it.
+//
+// Sharded k_step (OneshotArgs::compact): the words on the wire are a compact form of the
+// send buffer, 5x fewer at 8 ranks, since every word is stored once per rank over xGMI:
+//   [nR1]          R1 deltas, this rank's kDeltaReps replicas summed      (summed)
+//   [rows / 2]     this rank's part of every row word, 2 ints per word    (summed)
+//   [owned / 2]    this rank's block words only (owned block lb -> global
+//                  block rank + P lb), 2 ints per word                    (placed)
+//   [nR2 / 64]     R2New as bits instead of bytes                         (or-ed)
+// and the receiver writes recv in the send layout k_step reads (delta replica 0, the
+// row words, every rank's block words, R2New bytes 0/1); recv's other delta replicas
+// stay zero (begin() clears recv).
+constexpr int kOneshotChunks = 32;   // workgroups: each thread holds about one word or list entry
+struct OneshotCompact {
+    int nR1, rowOff, rowWords, cntOff, owned, nBlocks, newOff, newWords;   // u64 offsets and counts of send
+    int cR, cB, cN, total;                                                 // the compact layout
+};
 struct OneshotArgs {
     unsigned long long* inbox[kMaxRanks];
+    int compactOn;
+    OneshotCompact cx;
+    long long* tl;   // diagnostics: 8 stamps per workgroup (SBMP_TIMELINE_ITER), or null
 };
+
+// Compact word i of this rank (see above).
+__device__ __forceinline__ unsigned long long oneshot_pack(const OneshotCompact& x, const unsigned long long* send,
+                                                           int i, int rank, int nranks) {
+    if (i < x.cR) {
+        unsigned long long v = 0ull;
+#pragma unroll
+        for (int r = 0; r < kDeltaReps; ++r) v += send[(size_t)r * x.nR1 + i];
+        return v;
+    }
+    if (i < x.cB) return send[x.rowOff + (i - x.cR)];
+    if (i < x.cN) {
+        const int* cnt = reinterpret_cast<const int*>(send + x.cntOff);
+        const int lb = 2 * (i - x.cB);
+        const int g0 = rank + nranks * lb, g1 = g0 + nranks;
+        const unsigned lo = (lb < x.owned && g0 < x.nBlocks) ? (unsigned)cnt[g0] : 0u;
+        const unsigned hi = (lb + 1 < x.owned && g1 < x.nBlocks) ? (unsigned)cnt[g1] : 0u;
+        return ((unsigned long long)hi << 32) | lo;
+    }
+    const int w = i - x.cN;
+    unsigned long long bits = 0ull;
+#pragma unroll
+    for (int m = 0; m < 8; ++m) {   // 8 bytes -> 8 bits (bytes are 0 or 1; a nonzero byte is a set bit)
+        const int k = 8 * w + m;
+        const unsigned long long q = (k < x.newWords) ? send[x.newOff + k] : 0ull;
+        const unsigned long long hi = (((q & 0x7f7f7f7f7f7f7f7full) + 0x7f7f7f7f7f7f7f7full) | q) & 0x8080808080808080ull;
+        bits |= (((hi >> 7) * 0x0102040810204080ull) >> 56) << (8 * m);
+    }
+    return bits;
+}
+
+// Combine compact word i over the ranks' slots into recv (send layout).
+__device__ __forceinline__ void oneshot_unpack(const OneshotCompact& x, const unsigned long long* inbox, size_t slotStride,
+                                               unsigned long long* recv, int i, int nranks, int rank,
+                                               unsigned long long mine) {
+    unsigned long long v[kMaxRanks];
+#pragma unroll
+    for (int r = 0; r < kMaxRanks; ++r)
+        v[r] = (r == rank) ? mine
+               : (r < nranks) ? __hip_atomic_load(inbox + (size_t)r * slotStride + i, __ATOMIC_RELAXED,
+                                                  __HIP_MEMORY_SCOPE_SYSTEM)
+                              : 0ull;
+    if (i < x.cB) {   // deltas, rows: sums
+        unsigned long long s = 0ull;
+#pragma unroll
+        for (int r = 0; r < kMaxRanks; ++r) s += v[r];
+        recv[i < x.cR ? i : x.rowOff + (i - x.cR)] = s;
+    } else if (i < x.cN) {   // rank r's owned blocks lb, lb + 1 -> global blocks r + P lb
+        int* cnt = reinterpret_cast<int*>(recv + x.cntOff);
+        const int lb = 2 * (i - x.cB);
+        for (int r = 0; r < nranks; ++r) {
+            const int g0 = r + nranks * lb, g1 = g0 + nranks;
+            if (lb < x.owned && g0 < x.nBlocks) cnt[g0] = (int)(unsigned)v[r];
+            if (lb + 1 < x.owned && g1 < x.nBlocks) cnt[g1] = (int)(unsigned)(v[r] >> 32);
+        }
+    } else {   // R2New: or of the bits, back to bytes
+        unsigned long long bits = 0ull;
+#pragma unroll
+        for (int r = 0; r < kMaxRanks; ++r) bits |= v[r];
+        const int w = i - x.cN;
+#pragma unroll
+        for (int m = 0; m < 8; ++m) {
+            const int k = 8 * w + m;
+            if (k < x.newWords) {
+                const unsigned long long b8 = (bits >> (8 * m)) & 0xffull;   // bit b -> byte b (0 or 1)
+                const unsigned long long s = (b8 * 0x0101010101010101ull) & 0x8040201008040201ull;
+                recv[x.newOff + k] =
+                    ((((s & 0x7f7f7f7f7f7f7f7full) + 0x7f7f7f7f7f7f7f7full) | s) & 0x8080808080808080ull) >> 7;
+            }
+        }
+    }
+}
+
 // Chunk c of the exchange.
 __device__ __forceinline__ void oneshot_chunk(const OneshotArgs& a, const unsigned long long* __restrict__ send,
                                               unsigned long long* __restrict__ recv, long long n, int nranks,
                                               int rank, unsigned long long seq, int* error, int c) {
-    const long long per = (n + kOneshotChunks - 1) / kOneshotChunks;
-    const long long lo = c * per, hi = min(n, lo + per);
-    const size_t par = (size_t)(seq & 1ull) * nranks * n;
+    const int tid = (int)threadIdx.x;
+    long long* const tl = (a.tl && tid == 0 && c < 8) ? a.tl + (size_t)c * 8 : nullptr;   // chunks 0-7
+    if (tl) tl[0] = (long long)__builtin_amdgcn_s_memrealtime();
+    const long long nw = a.compactOn ? a.cx.total : n;   // words on the wire
+    const long long per = (nw + kOneshotChunks - 1) / kOneshotChunks;
+    const long long lo = c * per, hi = min(nw, lo + per);
+    const size_t par = (size_t)(seq & 1ull) * nranks * n;   // slots stay n words apart
     const size_t flags = (size_t)2 * nranks * n;
-    for (long long i = lo + threadIdx.x; i < hi; i += kBlock) {
-        const unsigned long long v = send[i];
+    // this rank's own slot is not stored: its words are recomputed from send below
+    for (long long i = lo + tid; i < hi; i += kBlock) {
+        const unsigned long long v = a.compactOn ? oneshot_pack(a.cx, send, (int)i, rank, nranks) : send[i];
         for (int q = 0; q < nranks; ++q)
-            __hip_atomic_store(a.inbox[q] + par + (size_t)rank * n + i, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            if (q != rank)
+                __hip_atomic_store(a.inbox[q] + par + (size_t)rank * n + i, v, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_SYSTEM);
     }
-    __threadfence_system();   // this thread's stores reach every rank before the flag
-    __syncthreads();
-    const int q = threadIdx.x;
-    if (q < nranks) {
-        __hip_atomic_store(a.inbox[q] + flags + (size_t)rank * kOneshotChunks + c, seq, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_SYSTEM);
-        unsigned long long* f = a.inbox[rank] + flags + (size_t)q * kOneshotChunks + c;
-        const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
-        while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < seq) {
-            if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > kExchangeWaitTicks) {   // report, do not hang
-                atomicExch(error, kErrExchange);
-                break;
+    if (tl) tl[1] = (long long)__builtin_amdgcn_s_memrealtime();
+    if (tl) tl[2] = (long long)__builtin_amdgcn_s_memrealtime();
+    if (nranks > 1) {
+        __threadfence_system();   // this thread's stores reach every rank before the flag
+        __syncthreads();
+        if (tl) tl[3] = (long long)__builtin_amdgcn_s_memrealtime();
+        if (tid < nranks && tid != rank) {   // raise flag (rank, c) at peer q, wait for (q, c) here
+            const int q = tid;
+            __hip_atomic_store(a.inbox[q] + flags + (size_t)rank * kOneshotChunks + c, seq, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_SYSTEM);
+            unsigned long long* f = a.inbox[rank] + flags + (size_t)q * kOneshotChunks + c;
+            const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
+            while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < seq) {
+                if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > kExchangeWaitTicks) {   // report, do not hang
+                    atomicExch(error, kErrExchange);
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(1);
             }
-            __builtin_amdgcn_s_sleep(1);
+        }
+        __threadfence_system();
+        __syncthreads();
+    }
+    if (tl) tl[4] = (long long)__builtin_amdgcn_s_memrealtime();
+    for (long long i = lo + tid; i < hi; i += kBlock) {
+        const unsigned long long mine = a.compactOn ? oneshot_pack(a.cx, send, (int)i, rank, nranks) : send[i];
+        if (a.compactOn) {
+            oneshot_unpack(a.cx, a.inbox[rank] + par, (size_t)n, recv, (int)i, nranks, rank, mine);
+        } else {
+            unsigned long long sum = mine;
+            for (int r = 0; r < nranks; ++r)
+                if (r != rank)
+                    sum += __hip_atomic_load(a.inbox[rank] + par + (size_t)r * n + i, __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_SYSTEM);
+            recv[i] = sum;
         }
     }
-    __threadfence_system();
-    __syncthreads();
-    for (long long i = lo + threadIdx.x; i < hi; i += kBlock) {
-        unsigned long long sum = 0ull;
-        for (int r = 0; r < nranks; ++r)
-            sum += __hip_atomic_load(a.inbox[rank] + par + (size_t)r * n + i, __ATOMIC_RELAXED,
-                                     __HIP_MEMORY_SCOPE_SYSTEM);
-        recv[i] = sum;
-    }
+    if (tl) tl[5] = (long long)__builtin_amdgcn_s_memrealtime();
 }
 
 __global__ __launch_bounds__(kBlock) void k_oneshot(OneshotArgs a, const unsigned long long* __restrict__ send,
@@ -847,7 +958,6 @@ __global__ __launch_bounds__(kBlock) void k_oneshot(OneshotArgs a, const unsigne
                                                     int rank, unsigned long long seq, int* error) {
     oneshot_chunk(a, send, recv, n, nranks, rank, seq, error, (int)blockIdx.x);
 }
-
 size_t oneshot_inbox_words(long long n, int nranks) { return (size_t)2 * nranks * n + (size_t)nranks * kOneshotChunks; }
 
 
@@ -946,6 +1056,7 @@ __device__ __forceinline__ void step_scan(const KgmtDev& d, int4 pk, int* sPfx, 
 // Sharded k_step: the scan runs over rows (block b of every rank), so its size is the
 // rank's block count however many ranks there are.  sPfx[r] = children of the rows
 // before r, *A the total, *gRow the lowest row holding a goal child (kNoGoalIdx if none).
+// One barrier, as step_scan: sPfx is written after it and needs the caller's next one.
 __device__ __forceinline__ void step_scan_rows(const KgmtDev& d, int4 pk, int* sPfx, int (*sRed)[kBlock / kWave],
                                                int* A, int* gRow) {
     const int tid = threadIdx.x;
@@ -962,19 +1073,19 @@ __device__ __forceinline__ void step_scan_rows(const KgmtDev& d, int4 pk, int* s
         if ((v4[e] >> 16) != 0 && grow == kNoGoalIdx) grow = tid * 4 + e;
     }
     const int incl = wave_incl_sum(run);
+    grow = first_lane_value(grow != kNoGoalIdx, grow, kNoGoalIdx);   // rows grow with the lane
     if (lane == kWave - 1) sRed[0][wave] = incl;
+    if (lane == 0) sRed[1][wave] = grow;
     __syncthreads();
-    int base = incl - run;
-    base += (wave > 0 ? sRed[0][0] : 0) + (wave > 1 ? sRed[0][1] : 0) + (wave > 2 ? sRed[0][2] : 0);
-    *A = __builtin_amdgcn_readfirstlane(sRed[0][0] + sRed[0][1] + sRed[0][2] + sRed[0][3]);
+    const int w0 = __builtin_amdgcn_readfirstlane(sRed[0][0]), w1 = __builtin_amdgcn_readfirstlane(sRed[0][1]),
+              w2 = __builtin_amdgcn_readfirstlane(sRed[0][2]), w3 = __builtin_amdgcn_readfirstlane(sRed[0][3]);
+    *A = w0 + w1 + w2 + w3;
+    *gRow = __builtin_amdgcn_readfirstlane(min(min(sRed[1][0], sRed[1][1]), min(sRed[1][2], sRed[1][3])));
+    const int base = incl - run + (wave > 0 ? w0 : 0) + (wave > 1 ? w1 : 0) + (wave > 2 ? w2 : 0);
 #pragma unroll
     for (int e = 0; e < 4; ++e)
         if (tid * 4 + e <= nRows) sPfx[tid * 4 + e] = base + loc[e];
     if (tid == kBlock - 1 && nRows == kMaxStepBlocks) sPfx[kMaxStepBlocks] = *A;
-    grow = first_lane_value(grow != kNoGoalIdx, grow, kNoGoalIdx);
-    if (lane == 0) sRed[1][wave] = grow;
-    __syncthreads();
-    *gRow = __builtin_amdgcn_readfirstlane(min(min(sRed[1][0], sRed[1][1]), min(sRed[1][2], sRed[1][3])));
 }
 
 // The P block words of row r (counts | (1 + goal index) << 16), in block order.
@@ -1018,16 +1129,22 @@ __device__ __forceinline__ int row_goal(const KgmtDev& d, const int* sPfx, int g
 // owner's (rank lo mod P, owned block lo / P) through its record buffer.
 template <bool SH>
 __device__ __forceinline__ const SBMP_GAS float4* list_entry(const KgmtDev& d, int pp, int lo, int i) {
-    if constexpr (SH)
+    if constexpr (SH) {
+        if (d.stepMirror)   // every rank's k_step pushed its lists here (uniform branch)
+            return G(d.stepMirror) + ((size_t)pp * d.nBlocks * kBlock + (size_t)lo * kBlock + i) * kStepEntry;
         return G(d.recPeer[lo % d.nranks]) +
                ((size_t)pp * d.recCap + (size_t)(lo / d.nranks) * kBlock + i) * kStepEntry;
-    else
+    } else {
         return G(d.stepList) + ((size_t)pp * d.nBlocks * kBlock + (size_t)lo * kBlock + i) * kStepEntry;
+    }
 }
+// Sharded lists in a peer's memory (mapped, no list mirror) take system-scope loads: this
+// GPU's L2 may hold their lines from two iterations ago.  The list mirror and a local
+// shard group's buffers are this GPU's memory written before this launch: plain loads.
 template <bool SH>
-__device__ __forceinline__ float4 list_load(const SBMP_GAS float4* p) {
-    if constexpr (SH) return load_record_g(p);   // peer memory, or lines cached two iterations ago
-    else return *p;
+__device__ __forceinline__ float4 list_load(const KgmtDev& d, const SBMP_GAS float4* p) {
+    if (SH && !d.listPlain) return load_record_g(p);
+    return *p;
 }
 
 // Plan scalars of iteration t from t-1's control block and the scan (KGMT.cu:118,
@@ -1157,6 +1274,7 @@ __device__ __forceinline__ void step_planner(const KgmtDev& d, int t, int expand
     if constexpr (SH) {
         int gRow;
         step_scan_rows(d, pk, sPfx, sRed, &A, &gRow);
+        if (gRow != kNoGoalIdx) __syncthreads();   // uniform (rare): row_goal reads sPfx[gRow]
         jGoal = row_goal(d, sPfx, gRow);
     } else {
         step_scan(d, pk, sPfx, sRed, &A, &jGoal);
@@ -1310,9 +1428,9 @@ __device__ __forceinline__ void step_planner(const KgmtDev& d, int t, int expand
             const int j1 = j0 + kBlock;
             const SBMP_GAS float4* e0 = entry(j0);
             const SBMP_GAS float4* e1 = entry(min(j1, n - 1));
-            const float4 s0 = list_load<SH>(e0), u0 = list_load<SH>(e0 + 1), s1 = list_load<SH>(e1),
-                         u1 = list_load<SH>(e1 + 1);
-            const float c0 = list_load<SH>(e0 + 2).x, c1 = list_load<SH>(e1 + 2).x;
+            const float4 s0 = list_load<SH>(d, e0), u0 = list_load<SH>(d, e0 + 1), s1 = list_load<SH>(d, e1),
+                         u1 = list_load<SH>(d, e1 + 1);
+            const float c0 = list_load<SH>(d, e0 + 2).x, c1 = list_load<SH>(d, e1 + 2).x;
             put(j0, s0, u0, c0);
             if (j1 < n) put(j1, s1, u1, c1);
         }
@@ -1438,18 +1556,19 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) voi
         return step_plan(d, t, expand, pcu, __builtin_amdgcn_readfirstlane(goalIdx), A, jGoal);
     };
     StepPlan q;
-    if constexpr (SH) {
-        int gRow;
-        step_scan_rows(d, pk, sPfx, sRed, &A, &gRow);
-        jGoal = row_goal(d, sPfx, gRow);
+    {
+        if constexpr (SH) {
+            int gRow;
+            step_scan_rows(d, pk, sPfx, sRed, &A, &gRow);
+            if (gRow != kNoGoalIdx) __syncthreads();   // uniform (rare): row_goal reads sPfx[gRow]
+            jGoal = row_goal(d, sPfx, gRow);
+        } else {
+            step_scan(d, pk, sPfx, sRed, &A, &jGoal);
+        }
         SBMP_STAMP(1);
-        q = plan();
-    } else {
         // One wave per workgroup computes the plan while the others write their prefix
         // entries; the barrier that publishes sPfx publishes the plan.  (Every wave
         // computing it kept the CU's one scalar unit busy for 16 waves at once.)
-        step_scan(d, pk, sPfx, sRed, &A, &jGoal);
-        SBMP_STAMP(1);
         if (wave == 0) {
             const StepPlan q0 = plan();
             if (lane == 0) sPlan = q0;
@@ -1487,9 +1606,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) voi
             const int dst = q.tsPrev + j;
             if (j < q.nIns && dst < d.M) {   // D13: the reference writes past M here
                 const SBMP_GAS float4* e = list_entry<SH>(d, pp, lo, tid);
-                const float4 s4 = list_load<SH>(e);
-                const float4 u4 = list_load<SH>(e + 1);
-                const float4 m4 = list_load<SH>(e + 2);
+                const float4 s4 = list_load<SH>(d, e);
+                const float4 u4 = list_load<SH>(d, e + 1);
+                const float4 m4 = list_load<SH>(d, e + 2);
                 G(d.treeState)[dst] = s4;
                 G(d.treeCtrl)[dst] = make_float4(u4.x, u4.y, u4.z, m4.x);   // cost = parent's + duration (KGMT.cu:631-633)
                 G(d.treeParent)[dst] = __float_as_int(u4.w);
@@ -1499,11 +1618,22 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) voi
     auto insert_prev = [&]() {
         if (t > 1 && selfInsert) {
             if constexpr (SH) {   // every rank holds the whole tree: row b = blocks b P .. b P + P - 1
-                int j0 = sPfx[b];
-                for (int r = 0; r < d.nranks; ++r) {
-                    const int c = rowW[r] & 0xffff;
-                    insert_block(b * d.nranks + r, j0, c);
-                    j0 += c;
+                // the row's entries over the workgroup's lanes (one round of loads for up to
+                // 256 entries, whichever of the P blocks holds them)
+                const int j0 = sPfx[b], tot = sPfx[b + 1] - j0;
+                for (int o = tid; o < tot; o += kBlock) {
+                    const int j = j0 + o, dst = q.tsPrev + j;
+                    if (j < q.nIns && dst < d.M) {   // D13: the reference writes past M here
+                        int blk, idx;
+                        row_locate(d, rowW, b, o, &blk, &idx);
+                        const SBMP_GAS float4* e = list_entry<SH>(d, pp, blk, idx);
+                        const float4 s4 = list_load<SH>(d, e);
+                        const float4 u4 = list_load<SH>(d, e + 1);
+                        const float4 m4 = list_load<SH>(d, e + 2);
+                        G(d.treeState)[dst] = s4;
+                        G(d.treeCtrl)[dst] = make_float4(u4.x, u4.y, u4.z, m4.x);
+                        G(d.treeParent)[dst] = __float_as_int(u4.w);
+                    }
                 }
             } else {
                 insert_block(b, sPfx[b], sPfx[b + 1] - sPfx[b]);
@@ -1519,7 +1649,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) voi
     // ---- expand t
     const bool act = slot < q.S;
     int g;   // slot = g*k + i
-    if (!SH && q.k >= kWave) {
+    if (q.k >= kWave) {
         const int2 gr = sWaveDiv[wave];
         g = gr.x + ((gr.y + lane >= q.k) ? 1 : 0);
     } else {
@@ -1581,7 +1711,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) voi
     // Parent and obstacles are issued back to back and waited for together.
     float4 p;
     float parentCost;
-    if (SH && fromList) {   // the owner's list: system-scope loads
+    if (SH && fromList && !d.listPlain) {   // the owner's list over the mapping: system-scope loads
         p = load_record_g(src);
         parentCost = load_record_g(src + 2).x;
     } else {
@@ -1723,11 +1853,25 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) voi
     const int c0 = sWaveCnt[0], c1 = sWaveCnt[1], c2 = sWaveCnt[2], c3 = sWaveCnt[3];
     const int waveOff = (wave > 0 ? c0 : 0) + (wave > 1 ? c1 : 0) + (wave > 2 ? c2 : 0);
     if (flagged) {
-        if constexpr (SH) {   // this rank's list of owned block b, written through for the peers
+        if constexpr (SH) {   // this rank's list of owned block b
             SBMP_GAS float4* e = G(d.recOut) + ((size_t)cp * d.recCap + (size_t)b * kBlock + waveOff + idxW) * kStepEntry;
-            store_record_g(e, cs);
-            store_record_g(e + 1, cc);
-            store_record_g(e + 2, make_float4(cost, 0.0f, 0.0f, 0.0f));
+            if (d.stepMirror) {   // into every rank's list mirror (global block gb), over xGMI for peers
+                const size_t m = ((size_t)cp * d.nBlocks * kBlock + (size_t)gb * kBlock + waveOff + idxW) * kStepEntry;
+                for (int q = 0; q < d.nranks; ++q) {
+                    SBMP_GAS float4* mq = G(d.mirrorPeer[q]) + m;
+                    store_record_g(mq, cs);
+                    store_record_g(mq + 1, cc);
+                    store_record_g(mq + 2, make_float4(cost, 0.0f, 0.0f, 0.0f));
+                }
+            } else if (d.listPlain) {   // read on this GPU after this launch (a local group)
+                e[0] = cs;
+                e[1] = cc;
+                e[2] = make_float4(cost, 0.0f, 0.0f, 0.0f);
+            } else {             // read by the peers over the mapping: written through
+                store_record_g(e, cs);
+                store_record_g(e + 1, cc);
+                store_record_g(e + 2, make_float4(cost, 0.0f, 0.0f, 0.0f));
+            }
         } else {
 #ifdef SBMP_SOFFSET_DEMO   // the round-3 form of these stores (kgmt_device.h, SBMP_WT_OFF)
             const __amdgpu_buffer_rsrc_t rl = wt_rsrc(d.stepList);
@@ -1978,7 +2122,7 @@ static void launch_step_form(const KgmtDev& d, int t, int expand, int variant, h
     const size_t shm = sizeof(float4) * (size_t)d.nObs + pfx;   // LDS obstacle forms
     const int blocks = SH ? d.nBlocks / d.nranks : d.nBlocks;
     const dim3 grid(1 + blocks), block(kBlock);   // workgroup 0 plans, 1.. expand
-    long long* const tlBase = (!SH && d.timeline && t == d.timelineIter && expand) ? d.timeline : nullptr;
+    long long* const tlBase = (d.timeline && t == d.timelineIter && expand) ? d.timeline : nullptr;
     const int4* const cnt4 = SH ? reinterpret_cast<const int4*>(d.stepXr + d.xRowOff)
                                 : reinterpret_cast<const int4*>(d.stepCnt + (size_t)((t - 1) & 1) * kMaxStepBlocks);
 #define SBMP_STEP_ARGS d.devSelf, t, expand, cnt4, d.ctrl + (t - 1), d.rngA, d.rngB, d.gnewOut, d.status, tlBase
@@ -2034,7 +2178,7 @@ static StepFn step_fn(const KgmtDev& d, int variant, size_t* shm) {
     return (variant == 2) ? k_step<AGENT, kObsLds4, SH> : k_step<AGENT, kObsLds, SH>;
 }
 
-int step_resident_groups(const KgmtDev& d, int agent, int variant) {
+int step_resident_groups(const KgmtDev& d, int agent, int variant, StepResidency* why) {
     size_t shm = 0;
     StepFn fn;
     if (agent == 0) fn = d.sharded ? step_fn<0, true>(d, variant, &shm) : step_fn<0, false>(d, variant, &shm);
@@ -2048,6 +2192,11 @@ int step_resident_groups(const KgmtDev& d, int agent, int variant) {
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&perCU, reinterpret_cast<const void*>(fn), kBlock, shm) !=
         hipSuccess)
         return 0;
+    if (why) {
+        why->perCU = perCU;
+        why->cus = cus;
+        why->dynLds = (long long)shm;
+    }
     return perCU * cus;
 }
 
@@ -2076,9 +2225,28 @@ void launch_fold_r2(const KgmtDev& d, int tFirst, int tLast, hipStream_t s, cons
 
 void launch_oneshot(unsigned long long* const* inbox, const unsigned long long* send, unsigned long long* recv,
                     long long n, int nranks, int rank, unsigned long long seq, int* error, hipStream_t s,
-                    const KernelTiming& tm) {
+                    const KernelTiming& tm, const OneshotLayout* compact,
+                    long long* tl) {
     OneshotArgs a{};
     for (int q = 0; q < nranks; ++q) a.inbox[q] = inbox[q];
+    if (compact && compact->on) {
+        OneshotCompact& x = a.cx;
+        a.compactOn = 1;
+        x.nR1 = compact->nR1;
+        x.rowOff = compact->rowOff;
+        x.rowWords = (compact->rows + 1) / 2;
+        x.cntOff = compact->cntOff;
+        x.owned = compact->owned;
+        x.nBlocks = compact->nBlocks;
+        x.newOff = compact->newOff;
+        x.newWords = compact->newWords;
+        x.cR = x.nR1;
+        x.cB = x.cR + x.rowWords;
+        x.cN = x.cB + (x.owned + 1) / 2;
+        x.total = x.cN + (x.newWords + 7) / 8;
+        if (x.total > n) a.compactOn = 0;   // cannot happen (the compact form is smaller); the full sum is exact too
+    }
+    a.tl = tl;
     launch(k_oneshot, dim3(kOneshotChunks), dim3(kBlock), 0, s, tm, a, send, recv, n, nranks, rank, seq, error);
 }
 

@@ -28,7 +28,11 @@ void launch_step(const KgmtDev& d, int t, int expand, int agent, int variant, hi
 // Workgroups of the k_step form launch_step would pick for d that the device holds at
 // once (occupancy per CU x CUs); k_step needs all of its 1 + blocks resident, since
 // its expanders wait for workgroup 0.  0 if the query fails.
-int step_resident_groups(const KgmtDev& d, int agent, int variant);
+struct StepResidency {   // the query's terms, for the message when k_step does not fit
+    int perCU = 0, cus = 0;
+    long long dynLds = 0;
+};
+int step_resident_groups(const KgmtDev& d, int agent, int variant, StepResidency* why = nullptr);
 void launch_fold_r2(const KgmtDev& d, int tFirst, int tLast, hipStream_t s, const KernelTiming& tm = KernelTiming());
 // k_finish(t): insert iteration t (insertBlocks = every global 256-slot block) +
 // prepare iteration t+1.  t = 0 prepares iteration 1 only (insertBlocks = 0).
@@ -41,9 +45,19 @@ void launch_pack(const KgmtDev& d, int t, int blocks, hipStream_t s, const Kerne
 // in the plan's lifetime (1, 2, ...), the same on every rank.
 size_t oneshot_inbox_words(long long n, int nranks);
 // error: the planner's status word (set to kErrExchange when a peer never arrives).
+// compact (sharded k_step): the send layout, sent in compact form (kgmt_kernels.hip).
+struct OneshotLayout {
+    int on;
+    int nR1;                  // R1 cells (kDeltaReps replicas of nR1 words at offset 0)
+    int rowOff, rows;         // u64 offset of the row words, rows (ints)
+    int cntOff, owned, nBlocks;   // u64 offset of the block words (ints), owned blocks, global blocks
+    int newOff, newWords;     // u64 offset and words of the R2New bytes
+};
+// tl: diagnostics, 8 stamps per workgroup, or null.
 void launch_oneshot(unsigned long long* const* inbox, const unsigned long long* send, unsigned long long* recv,
                     long long n, int nranks, int rank, unsigned long long seq, int* error, hipStream_t s,
-                    const KernelTiming& tm = KernelTiming());
+                    const KernelTiming& tm = KernelTiming(), const OneshotLayout* compact = nullptr,
+                    long long* tl = nullptr);
 // Local shard group: recv[q][i] = sum over ranks of send[r][i], for every rank q.
 void launch_xsum(const unsigned long long* const* send, unsigned long long* const* recv, int nranks, long long n,
                  hipStream_t s);

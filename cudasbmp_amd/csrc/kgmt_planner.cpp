@@ -219,6 +219,8 @@ KgmtPlanner::KgmtPlanner(const sbmp_kgmt_params& p, int nranks, int rank, Exchan
         d.stepXs[0] = shStep_ ? xSend_ : nullptr;
         d.stepXs[1] = shStep_ ? xSendOdd_ : nullptr;
         d.stepXr = shStep_ ? xRecv_ : nullptr;
+        d.stepMirror = nullptr;   // set below once the one-shot exchange is confirmed
+        d.listPlain = (sharded && !ex) ? 1 : 0;   // a local group: every rank's buffers are this GPU's
         d.xRowOff = (int)dWords;
         d.xCntOff = (int)(dWords + rowWords);
         d.xNewOff = (int)(dWords + rowWords + bcWords);
@@ -330,6 +332,26 @@ KgmtPlanner::KgmtPlanner(const sbmp_kgmt_params& p, int nranks, int rank, Exchan
                 fprintf(stderr, "sbmp: rank %d: the one-shot exchange failed its start-up check on this machine; "
                                 "the per-iteration exchange is the communicator's all-reduce\n", rank);
             }
+        }
+        // Sharded k_step + one-shot exchange: k_step pushes this rank's flagged-children
+        // lists into every rank's mirror (system-scope stores, over xGMI for the peers) and
+        // reads its parents from its own, in its own HBM, instead of the owners' record
+        // buffers over xGMI (SBMP_MIRROR=0: the remote reads).  A peer's stores are complete
+        // at the end of its k_step, before its k_oneshot raises the flags this rank's
+        // k_oneshot waits for; this rank's next k_step reads them after that kernel boundary,
+        // which refreshes this GPU's L2.  Parity t & 1 is rewritten in t + 2, after every
+        // rank's k_step(t + 1), the last reader, has ended (the exchange of t + 1 waits for it).
+        const char* cv = getenv("SBMP_ONESHOT_COMPACT");   // 0: the full send buffer on the wire
+        compactX_ = !(cv && atoi(cv) == 0);
+        const char* mv = getenv("SBMP_MIRROR");
+        if (oneshot_ && shStep_ && !(mv && atoi(mv) == 0)) {
+            const size_t bytes = sizeof(float4) * 2 * (size_t)d.nBlocks * kBlock * kStepEntry;
+            float4* own = alloc<float4>(bytes / sizeof(float4));
+            void* mp[kMaxRanks] = {nullptr};
+            ex_->share_buffer(own, bytes, mp);
+            for (int q = 0; q < nranks; ++q) d.mirrorPeer[q] = static_cast<float4*>(mp[q]);
+            d.stepMirror = own;
+            d.listPlain = 1;
         }
     }
 }
@@ -496,19 +518,31 @@ void KgmtPlanner::choose_form(const float* d_obstacles, int nObs) {
     // layout is k_step's); both are bit-exact for every list.
     d.stepMode = stepCapable_ ? 1 : 0;
     neededGroups_ = 1 + (d.sharded ? d.nBlocks / d.nranks : d.nBlocks);
-    residentGroups_ = stepCapable_ ? step_resident_groups(d, p_.agent, expandVariant_) : 0;
-    if (stepCapable_ && residentGroups_ < neededGroups_) {
+    StepResidency why;
+    residentGroups_ = stepCapable_ ? step_resident_groups(d, p_.agent, expandVariant_, &why) : 0;
+    // SBMP_STEP_RESIDENCY=warn: sharded ranks that share one GPU (a rehearsal on one
+    // device), where the query answers for the device the other processes hold too
+    const char* rv = getenv("SBMP_STEP_RESIDENCY");
+    const bool warnOnly = d.sharded && rv && std::string(rv) == "warn";
+    if (stepCapable_ && residentGroups_ < neededGroups_ && warnOnly) {
+        if (!formLogged_)
+            fprintf(stderr, "sbmp: rank %d: k_step needs %d resident workgroups, the occupancy query gives %d "
+                            "(%d per CU x %d CUs); SBMP_STEP_RESIDENCY=warn: launching it as is\n",
+                    d.rank, neededGroups_, residentGroups_, why.perCU, why.cus);
+        formLogged_ = true;
+    } else if (stepCapable_ && residentGroups_ < neededGroups_) {
         const int before = residentGroups_;
         if (!d.sharded) {
             d.stepMode = 0;
         } else if (!d.gridStart && nObs > 0) {
             build_grid(d_obstacles, nObs);
-            residentGroups_ = step_resident_groups(d, p_.agent, expandVariant_);
+            residentGroups_ = step_resident_groups(d, p_.agent, expandVariant_, &why);
         }
         if (d.sharded && residentGroups_ < neededGroups_)
-            throw Error(SBMP_ERR_INVALID_ARGUMENT, "k_step needs " + std::to_string(neededGroups_) +
-                                                       " resident workgroups per rank; the device holds " +
-                                                       std::to_string(residentGroups_));
+            throw Error(SBMP_ERR_INVALID_ARGUMENT,
+                        "k_step needs " + std::to_string(neededGroups_) + " resident workgroups per rank; the device holds " +
+                            std::to_string(residentGroups_) + " (" + std::to_string(why.perCU) + " per CU x " +
+                            std::to_string(why.cus) + " CUs at " + std::to_string(why.dynLds) + " B of dynamic LDS)");
         if (!formLogged_) {
             fprintf(stderr, "sbmp: %d obstacles: k_step needs %d workgroups resident, the device holds %d; %s\n", nObs,
                     neededGroups_, before,
@@ -531,6 +565,7 @@ void KgmtPlanner::path_info(sbmp_path_info* out) {
     out->nranks = d.nranks;
     out->rank = d.rank;
     out->commRanks = ex_ ? ex_->comm_ranks() : 0;
+    out->listMirror = d.stepMirror ? 1 : 0;
 }
 
 void KgmtPlanner::build_grid(const float* d_obstacles, int nObs) {
@@ -614,8 +649,21 @@ void KgmtPlanner::stage_exchange(int t) {
     const unsigned long long* send = exchange_send(t);
     if (oneshot_) {
         ++xSeq_;
+        OneshotLayout cx{};
+        if (shStep_ && compactX_) {   // the sharded k_step layout, compact on the wire
+            cx.on = 1;
+            cx.nR1 = d_.nR1;
+            cx.rowOff = d_.xRowOff;
+            cx.rows = expandBlocks_;
+            cx.cntOff = d_.xCntOff;
+            cx.owned = expandBlocks_;
+            cx.nBlocks = d_.nBlocks;
+            cx.newOff = d_.xNewOff;
+            cx.newWords = (int)xWords_ - d_.xNewOff;
+        }
+        long long* tl = (d_.timelineFin && t == d_.timelineIter) ? d_.timelineFin + kTimelineStamps : nullptr;
         launch_oneshot(inbox_, send, xRecv_, (long long)xWords_, d_.nranks, d_.rank, xSeq_, &d_.status->error,
-                       stream_, timing(K_XCHG));
+                       stream_, timing(K_XCHG), &cx, tl);
     } else {
         ex_->allreduce_u64(send, xRecv_, xWords_, stream_);
     }
@@ -667,7 +715,8 @@ void KgmtPlanner::sync() {
         const size_t nf = (size_t)(1 + d_.nBlocks) * kTimelineStamps;
         std::vector<long long> h(n + nf);
         SBMP_HIP(hipMemcpy(h.data(), d_.timeline, sizeof(long long) * (n + nf), hipMemcpyDeviceToHost));
-        const std::string path = getenv("SBMP_TIMELINE_OUT") ? getenv("SBMP_TIMELINE_OUT") : "sbmp_timeline.bin";
+        std::string path = getenv("SBMP_TIMELINE_OUT") ? getenv("SBMP_TIMELINE_OUT") : "sbmp_timeline.bin";
+        if (d_.nranks > 1) path += ".r" + std::to_string(d_.rank);   // a local group's ranks share the process
         if (FILE* f = fopen(path.c_str(), "wb")) {
             fwrite(h.data(), sizeof(long long), n, f);
             fclose(f);

@@ -205,6 +205,7 @@ private:
     bool oneshot_ = false;                   // sharded: the exchange is k_oneshot over IPC-mapped inboxes
     bool oneshot_self_test();                // k_oneshot checked once at construction (all ranks agree)
     unsigned long long* inbox_[kMaxRanks] = {nullptr};
+    bool compactX_ = true;   // sharded k_step: k_oneshot sends the compact form of the exchange   // every rank's list mirror (sharded k_step, one-shot)
     unsigned long long xSeq_ = 0;            // exchanges so far (the same count on every rank)
     uint32_t* jumps_ = nullptr;
     float4* obs_ = nullptr;

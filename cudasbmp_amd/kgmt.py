@@ -332,7 +332,8 @@ class KGMT:
                 "obstacle_form": self.OBSTACLE_FORMS[pi.obstacleForm] if 0 <= pi.obstacleForm < 4 else pi.obstacleForm,
                 "resident_groups": pi.residentGroups, "needed_groups": pi.neededGroups,
                 "exchange": self.EXCHANGES[pi.exchange] if 0 <= pi.exchange < 3 else pi.exchange,
-                "nranks": pi.nranks, "rank": pi.rank, "rccl_nranks": pi.commRanks}
+                "nranks": pi.nranks, "rank": pi.rank, "rccl_nranks": pi.commRanks,
+                "list_mirror": bool(pi.listMirror)}
 
     def kernel_samples(self, name: str) -> np.ndarray:
         """Per-launch durations (ms) of kernel `name` since the last reset_kernel_stats()."""

@@ -112,6 +112,8 @@ typedef struct sbmp_path_info {
     int exchange;             /* SBMP_EXCHANGE_* */
     int nranks, rank;
     int commRanks;            /* ranks of the RCCL communicator (0: none) */
+    int listMirror;           /* 1: the one-shot exchange copies the flagged-children lists into each
+                                 rank's mirror, and k_step reads its parents from local HBM */
 } sbmp_path_info;
 
 typedef struct sbmp_kgmt sbmp_kgmt;

@@ -52,6 +52,15 @@ def main():
         t0w = a[a[:, 6] != 0, 0].min()
         print(f"planner: entry {(f[0] - t0w) / 100.0:+.2f} us, publish {(f[1] - t0w) / 100.0:+.2f} us "
               f"(relative to the first expanding wave's entry)")
+        ex = f[8:8 + 64].reshape(8, 8)   # k_oneshot of the same iteration (sharded ranks), one row per chunk
+        if (ex[:, 0] != 0).any():
+            t_end = a[a[:, 6] != 0, 6].max()
+            print("k_oneshot chunks (us after the last k_step wave's end):  entry  stored  mirror  fenced  "
+                  "flags   end")
+            for c in range(8):
+                if ex[c, 0]:
+                    print(f"  chunk {c}                                                " +
+                          " ".join(f"{(ex[c, i] - t_end) / 100.0:7.2f}" for i in range(6)))
     live = a[a[:, 6] != 0]
     print(f"{len(a)} waves, {len(live)} ran the full path")
     t0 = live[:, 0].min()
