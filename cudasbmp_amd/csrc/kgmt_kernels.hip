@@ -1057,12 +1057,20 @@ __device__ __forceinline__ void step_scan(const KgmtDev& d, int4 pk, int* sPfx, 
 // rank's block count however many ranks there are.  sPfx[r] = children of the rows
 // before r, *A the total, *gRow the lowest row holding a goal child (kNoGoalIdx if none).
 // One barrier, as step_scan: sPfx is written after it and needs the caller's next one.
-__device__ __forceinline__ void step_scan_rows(const KgmtDev& d, int4 pk, int* sPfx, int (*sRed)[kBlock / kWave],
+// A sharded rank's geometry for k_step, from kernel arguments: they arrive with the
+// first batch of argument loads, where the same fields of the plan struct took two more
+// dependent scalar round trips in front of the prologue's loads.
+struct ShardView {
+    int nranks, rank, nRows;    // ranks, this rank, rows (owned blocks)
+    const SBMP_GAS int* bw;     // the exchange's block words (stepXr + xCntOff)
+};
+
+__device__ __forceinline__ void step_scan_rows(const ShardView& sv, int4 pk, int* sPfx, int (*sRed)[kBlock / kWave],
                                                int* A, int* gRow) {
     const int tid = threadIdx.x;
     const int lane = tid & (kWave - 1);
     const int wave = tid >> 6;
-    const int nRows = d.nBlocks / d.nranks;
+    const int nRows = sv.nRows;
     int loc[4];
     int run = 0, grow = kNoGoalIdx;
     const int v4[4] = {pk.x, pk.y, pk.z, pk.w};
@@ -1088,37 +1096,44 @@ __device__ __forceinline__ void step_scan_rows(const KgmtDev& d, int4 pk, int* s
     if (tid == kBlock - 1 && nRows == kMaxStepBlocks) sPfx[kMaxStepBlocks] = *A;
 }
 
-// The P block words of row r (counts | (1 + goal index) << 16), in block order.
-__device__ __forceinline__ void row_words(const KgmtDev& d, int r, int* w) {
-    const SBMP_GAS int* blk = reinterpret_cast<const SBMP_GAS int*>(G(d.stepXr) + d.xCntOff) + (size_t)r * d.nranks;
+// The P block words of row r (counts | (1 + goal index) << 16), in block order.  All
+// kMaxRanks words are loaded unconditionally (one batch, no load behind a branch: the
+// conditional form became a chain of scalar loads, each waited for before the next);
+// the ones past row r's P lie inside the exchange buffer (the block words of row r + 1,
+// or the R2New bytes after them) and are masked.
+__device__ __forceinline__ void row_words(const ShardView& sv, int r, int* w) {
+    const SBMP_GAS int* blk = sv.bw + (size_t)r * sv.nranks;
+    int v[kMaxRanks];
 #pragma unroll
-    for (int q = 0; q < kMaxRanks; ++q) w[q] = (q < d.nranks) ? blk[q] : 0;
+    for (int q = 0; q < kMaxRanks; ++q) v[q] = blk[q];
+#pragma unroll
+    for (int q = 0; q < kMaxRanks; ++q) w[q] = (q < sv.nranks) ? v[q] : 0;
 }
 
 // Position off inside row r -> (global block, index in it), from the row's words.
-__device__ __forceinline__ void row_locate(const KgmtDev& d, const int* w, int r, int off, int* block, int* idx) {
+__device__ __forceinline__ void row_locate(const ShardView& sv, const int* w, int r, int off, int* block, int* idx) {
     int q = 0;
 #pragma unroll
     for (int k = 0; k < kMaxRanks - 1; ++k) {
         const int c = w[k] & 0xffff;
-        if (k == q && k + 1 < d.nranks && off >= c) {
+        if (k == q && k + 1 < sv.nranks && off >= c) {
             off -= c;
             q = k + 1;
         }
     }
-    *block = r * d.nranks + q;
+    *block = r * sv.nranks + q;
     *idx = off;
 }
 
 // jGoal of a sharded scan: the lowest global index of a goal child, in row gRow.
-__device__ __forceinline__ int row_goal(const KgmtDev& d, const int* sPfx, int gRow) {
+__device__ __forceinline__ int row_goal(const ShardView& sv, const int* sPfx, int gRow) {
     if (gRow == kNoGoalIdx) return kNoGoalIdx;
     int w[kMaxRanks];
-    row_words(d, gRow, w);
+    row_words(sv, gRow, w);
     int pre = sPfx[gRow], j = kNoGoalIdx;
 #pragma unroll
     for (int q = 0; q < kMaxRanks; ++q) {
-        if (q < d.nranks && j == kNoGoalIdx && (w[q] >> 16) != 0) j = pre + (w[q] >> 16) - 1;
+        if (q < sv.nranks && j == kNoGoalIdx && (w[q] >> 16) != 0) j = pre + (w[q] >> 16) - 1;
         pre += w[q] & 0xffff;
     }
     return __builtin_amdgcn_readfirstlane(j);
@@ -1205,7 +1220,7 @@ __device__ __forceinline__ StepPlan step_plan(const KgmtDev& d, int t, int expan
 // = the snapshot, R1Cov), scores (updateR1, KGMT.cu:485-538, CUB order D8), ctrl[t];
 // scores and snapshot published as 8-B words tagged with t.
 template <bool SH>
-__device__ __forceinline__ void step_planner(const KgmtDev& d, int t, int expand, int* sPfx,
+__device__ __forceinline__ void step_planner(const KgmtDev& d, const ShardView& sv, int t, int expand, int* sPfx,
                                              int (*sRed)[kBlock / kWave], int* sCovInc, float* sPart) {
     constexpr int kW = kMaxR2Words / kBlock;
     const int tid = threadIdx.x;
@@ -1273,9 +1288,9 @@ __device__ __forceinline__ void step_planner(const KgmtDev& d, int t, int expand
     int A, jGoal;
     if constexpr (SH) {
         int gRow;
-        step_scan_rows(d, pk, sPfx, sRed, &A, &gRow);
+        step_scan_rows(sv, pk, sPfx, sRed, &A, &gRow);
         if (gRow != kNoGoalIdx) __syncthreads();   // uniform (rare): row_goal reads sPfx[gRow]
-        jGoal = row_goal(d, sPfx, gRow);
+        jGoal = row_goal(sv, sPfx, gRow);
     } else {
         step_scan(d, pk, sPfx, sRed, &A, &jGoal);
     }
@@ -1404,15 +1419,15 @@ __device__ __forceinline__ void step_planner(const KgmtDev& d, int t, int expand
     if (t > 1 && A <= kPlannerInsertMax) {
         const int n = min(q.nIns, d.M - q.tsPrev);   // D13: the reference writes past M
         // list entry of row j: block (sharded: row) lo with sPfx[lo] <= j < sPfx[lo + 1]
-        const int nS = SH ? d.nBlocks / d.nranks : d.nBlocks;
+        const int nS = SH ? sv.nRows : d.nBlocks;
         auto entry = [&](int j) {
             int lo = 0;
             for (int step = kMaxStepBlocks / 2; step > 0; step >>= 1)
                 if (lo + step < nS && sPfx[lo + step] <= j) lo += step;
             if constexpr (SH) {
                 int w[kMaxRanks], blk, idx;
-                row_words(d, lo, w);
-                row_locate(d, w, lo, j - sPfx[lo], &blk, &idx);
+                row_words(sv, lo, w);
+                row_locate(sv, w, lo, j - sPfx[lo], &blk, &idx);
                 return list_entry<SH>(d, pp, blk, idx);
             } else {
                 return list_entry<SH>(d, pp, lo, j - sPfx[lo]);
@@ -1463,8 +1478,10 @@ template <int AGENT, int OBS, bool SH>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) void k_step(
     const KgmtDev* __restrict__ dp, int t, int expand, const int4* __restrict__ cnt4,
     const IterCtrl* __restrict__ ctrlPrev, const uint4* __restrict__ rngAArg, const uint2* __restrict__ rngBArg,
-    const unsigned long long* __restrict__ gnewArg, const PlannerStatus* __restrict__ statusArg, long long* tlBase) {
+    const unsigned long long* __restrict__ gnewArg, const PlannerStatus* __restrict__ statusArg, long long* tlBase,
+    int shRanks, int shRank, int shRows, const int* __restrict__ shBw) {
     const KgmtDev& d = *dp;
+    const ShardView sv{SH ? shRanks : 1, SH ? shRank : 0, SH ? shRows : 0, G(shBw)};
     extern __shared__ float4 sDyn[];   // [LDS obstacles][prefix: nBlocks + 1 ints][R2New bits: nR2 / 32]
     __shared__ int sR1P[kMaxR1];
     __shared__ StepPlan sPlan;
@@ -1477,9 +1494,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) voi
     constexpr bool kLdsObs = (OBS == kObsLds || OBS == kObsLds4);
     constexpr int kRegObs = obs_in_registers(OBS);
     int* const sPfx = reinterpret_cast<int*>(sDyn + (kLdsObs ? d.nObs : 0));
-    uint32_t* const sNew = reinterpret_cast<uint32_t*>(sPfx + (SH ? d.nBlocks / d.nranks : d.nBlocks) + 1);
+    uint32_t* const sNew = reinterpret_cast<uint32_t*>(sPfx + (SH ? sv.nRows : d.nBlocks) + 1);
     if (blockIdx.x == 0) {
-        step_planner<SH>(d, t, expand, sPfx, sRed, sCovInc, sPart);
+        step_planner<SH>(d, sv, t, expand, sPfx, sRed, sCovInc, sPart);
         return;
     }
     float4* const sObs = sDyn;
@@ -1488,7 +1505,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) voi
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // uniform
     __shared__ int2 sWaveDiv[kBlock / kWave];   // (frontier position, remainder) of each wave's first slot
     const int b = (int)blockIdx.x - 1;                // this workgroup's 256-slot block (owned index)
-    const int gb = SH ? d.rank + d.nranks * b : b;   // global block
+    const int gb = SH ? sv.rank + sv.nranks * b : b;   // global block
     const int slot = gb * kBlock + tid;
     const int nW = d.nR2 >> 5;
     const int pp = (t - 1) & 1, cp = t & 1;
@@ -1523,7 +1540,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) voi
     const int4 pk = G(cnt4)[tid];
     const IterCtrl pc = *ctrlP;
     int rowW[SH ? kMaxRanks : 1];   // sharded: the block words of this workgroup's row (its inserts)
-    if constexpr (SH) row_words(d, b, rowW);
+    if constexpr (SH) row_words(sv, b, rowW);
     const int goalIdx = statusP->goalIdx;
     const uint4 ra = rngAP[slot];
     const uint2 rb = rngBP[slot];
@@ -1559,9 +1576,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) voi
     {
         if constexpr (SH) {
             int gRow;
-            step_scan_rows(d, pk, sPfx, sRed, &A, &gRow);
+            step_scan_rows(sv, pk, sPfx, sRed, &A, &gRow);
             if (gRow != kNoGoalIdx) __syncthreads();   // uniform (rare): row_goal reads sPfx[gRow]
-            jGoal = row_goal(d, sPfx, gRow);
+            jGoal = row_goal(sv, sPfx, gRow);
         } else {
             step_scan(d, pk, sPfx, sRed, &A, &jGoal);
         }
@@ -1625,7 +1642,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) voi
                     const int j = j0 + o, dst = q.tsPrev + j;
                     if (j < q.nIns && dst < d.M) {   // D13: the reference writes past M here
                         int blk, idx;
-                        row_locate(d, rowW, b, o, &blk, &idx);
+                        row_locate(sv, rowW, b, o, &blk, &idx);
                         const SBMP_GAS float4* e = list_entry<SH>(d, pp, blk, idx);
                         const float4 s4 = list_load<SH>(d, e);
                         const float4 u4 = list_load<SH>(d, e + 1);
@@ -1671,7 +1688,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) voi
         const int jA = __builtin_amdgcn_readlane(j, (int)__builtin_ctzll(need));
         const int jB = __builtin_amdgcn_readlane(j, 63 - (int)__builtin_clzll(need));
         int lo = 0;
-        const int nS = SH ? d.nBlocks / d.nranks : d.nBlocks;   // scan entries: blocks, or (sharded) rows
+        const int nS = SH ? sv.nRows : d.nBlocks;   // scan entries: blocks, or (sharded) rows
         if (jB - jA <= 1) {
             const int jj = (lane < 32) ? jA : jB;
             const int sub = lane & 31;
@@ -1699,8 +1716,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) voi
         if (fromList) {
             if constexpr (SH) {   // the row's blocks: one more (L2) round trip for their words
                 int w[kMaxRanks], blk, idx;
-                row_words(d, lo, w);
-                row_locate(d, w, lo, j - sPfx[lo], &blk, &idx);
+                row_words(sv, lo, w);
+                row_locate(sv, w, lo, j - sPfx[lo], &blk, &idx);
                 src = list_entry<SH>(d, pp, blk, idx);
             } else {
                 src = list_entry<SH>(d, pp, lo, j - sPfx[lo]);
@@ -1768,8 +1785,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) voi
         // brings it into that XCD's L2 and later waves hit there instead of each going
         // to memory; a line loaded before publication carries an older tag, and the
         // re-read below (agent scope, past this CU's caches) corrects it.
-        sw = pubCur[q1];
-        aw = pubCur[d.nR1 + (q2 >> 5)];
+        // (relaxed atomic loads at workgroup scope: the same plain, cacheable global_load,
+        // without the data race a plain load of a word another workgroup stores would be)
+        sw = __hip_atomic_load(pubCur + q1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        aw = __hip_atomic_load(pubCur + d.nR1 + (q2 >> 5), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
     float u = 0.0f;
     if (valid) u = xorwow_uniform(rs);   // KGMT.cu:395 (valid implies act)
@@ -1857,7 +1876,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) voi
             SBMP_GAS float4* e = G(d.recOut) + ((size_t)cp * d.recCap + (size_t)b * kBlock + waveOff + idxW) * kStepEntry;
             if (d.stepMirror) {   // into every rank's list mirror (global block gb), over xGMI for peers
                 const size_t m = ((size_t)cp * d.nBlocks * kBlock + (size_t)gb * kBlock + waveOff + idxW) * kStepEntry;
-                for (int q = 0; q < d.nranks; ++q) {
+                for (int q = 0; q < sv.nranks; ++q) {
                     SBMP_GAS float4* mq = G(d.mirrorPeer[q]) + m;
                     store_record_g(mq, cs);
                     store_record_g(mq + 1, cc);
@@ -2125,7 +2144,10 @@ static void launch_step_form(const KgmtDev& d, int t, int expand, int variant, h
     long long* const tlBase = (d.timeline && t == d.timelineIter && expand) ? d.timeline : nullptr;
     const int4* const cnt4 = SH ? reinterpret_cast<const int4*>(d.stepXr + d.xRowOff)
                                 : reinterpret_cast<const int4*>(d.stepCnt + (size_t)((t - 1) & 1) * kMaxStepBlocks);
-#define SBMP_STEP_ARGS d.devSelf, t, expand, cnt4, d.ctrl + (t - 1), d.rngA, d.rngB, d.gnewOut, d.status, tlBase
+#define SBMP_STEP_ARGS                                                                                      \
+    d.devSelf, t, expand, cnt4, d.ctrl + (t - 1), d.rngA, d.rngB, d.gnewOut, d.status, tlBase, SH ? d.nranks : 1, \
+        SH ? d.rank : 0, SH ? d.nBlocks / d.nranks : d.nBlocks,                                                   \
+        SH ? reinterpret_cast<const int*>(d.stepXr + d.xCntOff) : nullptr
     if (d.gridStart) {
         launch(k_step<AGENT, kObsGrid, SH>, grid, block, pfx, s, tm, SBMP_STEP_ARGS);
     } else if (d.nObs > kMaxLdsObs) {
@@ -2153,7 +2175,7 @@ static void launch_step_form(const KgmtDev& d, int t, int expand, int variant, h
 // The k_step instantiation launch_step_form picks, and its dynamic LDS, for the
 // residency check (step_resident_groups).
 using StepFn = void (*)(const KgmtDev*, int, int, const int4*, const IterCtrl*, const uint4*, const uint2*,
-                        const unsigned long long*, const PlannerStatus*, long long*);
+                        const unsigned long long*, const PlannerStatus*, long long*, int, int, int, const int*);
 template <int AGENT, bool SH>
 static StepFn step_fn(const KgmtDev& d, int variant, size_t* shm) {
     const size_t nS = SH ? d.nBlocks / d.nranks : d.nBlocks;

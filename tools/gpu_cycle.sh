@@ -58,10 +58,10 @@ sq)
     timeout -k 10 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM SQ_WAVE_CYCLES \
         SQ_BUSY_CYCLES SQ_WAIT_INST_ANY -d "$R/$out/sq" -o run --output-format csv -- python3 "$R/bench.py" \
         --steps 30 --warmup 20 --no-cpu-baseline --no-ttfs "$@" > "$R/$out/sq.log" 2>&1 || exit 1
-    cd "$R" && python3 tools/pmc_summary.py "$out" --skip 25 | head -20 ;;
+    cd "$R" && python3 tools/pmc_summary.py "$out" --skip 25 > "$R/$out/sq_summary.txt" && sed -n 1,30p "$R/$out/sq_summary.txt" ;;
 pmc)
     bash tools/profile_pmc.sh "$out" "$@" || exit 1
-    python3 tools/pmc_summary.py "$out" --skip 25 | head -30 ;;
+    python3 tools/pmc_summary.py "$out" --skip 25 > "$R/$out/pmc_summary.txt" && sed -n 1,40p "$R/$out/pmc_summary.txt" ;;
 trace)
     cd /tmp && export TMPDIR=/tmp
     timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$R/$out/trace" -o run --output-format csv -- \
