@@ -103,6 +103,16 @@ constexpr int kInsertBase = 8;   // k_finish workgroup of insert block 0 (one pe
 constexpr int kRecordF4 = 3;   // sharded record: state, ctrl (a, steer, dur, parent), (block, index in block, -, -)
 
 // Everything a kernel needs, passed by value.
+// The compact form of the sharded k_step's exchange (k_oneshot, and k_step's own tail
+// when the exchange is fused; kgmt_kernels.hip): u64 offsets and counts of the send
+// buffer, then the compact layout's region starts and total.
+constexpr int kFxCounters = 9;   // fused exchange: 8 arrival shards + the top counter
+constexpr int kFxStride = 32;    // u32 words between counters (128 B)
+struct OneshotCompact {
+    int nR1, rowOff, rowWords, cntOff, owned, nBlocks, newOff, newWords;
+    int cR, cB, cN, total;
+};
+
 struct KgmtDev {
     int M, nSlots, nWords, nBlocks, numIterations, numDisc, N, n, nR1, nR2, nObs, cap, fixGNewClear;
     int batchRule;        // 0 = reference rule (+ cap), 1 = fill the cap (D14)
@@ -201,6 +211,18 @@ struct KgmtDev {
     // the lists are read from the owners' record buffers)
     float4* stepMirror;
     float4* mirrorPeer[kMaxRanks];   // every rank's stepMirror, mapped here
+    // Fused exchange (sharded k_step + one-shot exchange + list mirror): the last
+    // expanding workgroup of k_step(t) runs the exchange of t itself (k_step_exchange),
+    // instead of a k_oneshot launch.  xInbox: every rank's inbox, mapped here;
+    // xArrive: [2 parities][kFxCounters][kFxStride] arrival counters (8 shards by block
+    // index, then the top counter, each on a 128-B line); exchange t has sequence number
+    // xSeqBase + t.
+    int fusedX;
+    int xInboxWords;   // n of the inbox layout (slot stride)
+    unsigned long long* xInbox[kMaxRanks];
+    unsigned* xArrive;
+    unsigned long long xSeqBase;
+    OneshotCompact xc;
     int listPlain;   // sharded lists readable with plain loads (the mirror, or a local shard group)
     int xRowOff, xCntOff, xNewOff;   // u64 offsets of the row words, block words and R2New bytes
     // k_step reads this struct from device memory (a copy the host refreshes before a

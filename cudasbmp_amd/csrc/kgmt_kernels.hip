@@ -810,10 +810,6 @@ __global__ __launch_bounds__(kBlock) void k_finish(KgmtDev d, int t) {
 // row words, every rank's block words, R2New bytes 0/1); recv's other delta replicas
 // stay zero (begin() clears recv).
 constexpr int kOneshotChunks = 32;   // workgroups: each thread holds about one word or list entry
-struct OneshotCompact {
-    int nR1, rowOff, rowWords, cntOff, owned, nBlocks, newOff, newWords;   // u64 offsets and counts of send
-    int cR, cB, cN, total;                                                 // the compact layout
-};
 struct OneshotArgs {
     unsigned long long* inbox[kMaxRanks];
     int compactOn;
@@ -822,21 +818,34 @@ struct OneshotArgs {
 };
 
 // Compact word i of this rank (see above).
+// SC1: every load of send is an agent-scope (sc1) load, for the fused exchange, which
+// reads what other workgroups of the same launch wrote through (k_step's tail).
+template <bool SC1 = false>
+__device__ __forceinline__ unsigned long long send_u64(const unsigned long long* p) {
+    if constexpr (SC1) return __hip_atomic_load(G(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else return *p;
+}
+template <bool SC1 = false>
+__device__ __forceinline__ unsigned send_u32(const int* p) {
+    if constexpr (SC1) return (unsigned)__hip_atomic_load(G(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else return (unsigned)*p;
+}
+template <bool SC1 = false>
 __device__ __forceinline__ unsigned long long oneshot_pack(const OneshotCompact& x, const unsigned long long* send,
                                                            int i, int rank, int nranks) {
     if (i < x.cR) {
         unsigned long long v = 0ull;
 #pragma unroll
-        for (int r = 0; r < kDeltaReps; ++r) v += send[(size_t)r * x.nR1 + i];
+        for (int r = 0; r < kDeltaReps; ++r) v += send_u64<SC1>(send + (size_t)r * x.nR1 + i);
         return v;
     }
-    if (i < x.cB) return send[x.rowOff + (i - x.cR)];
+    if (i < x.cB) return send_u64<SC1>(send + x.rowOff + (i - x.cR));
     if (i < x.cN) {
         const int* cnt = reinterpret_cast<const int*>(send + x.cntOff);
         const int lb = 2 * (i - x.cB);
         const int g0 = rank + nranks * lb, g1 = g0 + nranks;
-        const unsigned lo = (lb < x.owned && g0 < x.nBlocks) ? (unsigned)cnt[g0] : 0u;
-        const unsigned hi = (lb + 1 < x.owned && g1 < x.nBlocks) ? (unsigned)cnt[g1] : 0u;
+        const unsigned lo = (lb < x.owned && g0 < x.nBlocks) ? send_u32<SC1>(cnt + g0) : 0u;
+        const unsigned hi = (lb + 1 < x.owned && g1 < x.nBlocks) ? send_u32<SC1>(cnt + g1) : 0u;
         return ((unsigned long long)hi << 32) | lo;
     }
     const int w = i - x.cN;
@@ -844,7 +853,7 @@ __device__ __forceinline__ unsigned long long oneshot_pack(const OneshotCompact&
 #pragma unroll
     for (int m = 0; m < 8; ++m) {   // 8 bytes -> 8 bits (bytes are 0 or 1; a nonzero byte is a set bit)
         const int k = 8 * w + m;
-        const unsigned long long q = (k < x.newWords) ? send[x.newOff + k] : 0ull;
+        const unsigned long long q = (k < x.newWords) ? send_u64<SC1>(send + x.newOff + k) : 0ull;
         const unsigned long long hi = (((q & 0x7f7f7f7f7f7f7f7full) + 0x7f7f7f7f7f7f7f7full) | q) & 0x8080808080808080ull;
         bits |= (((hi >> 7) * 0x0102040810204080ull) >> 56) << (8 * m);
     }
@@ -958,6 +967,112 @@ __global__ __launch_bounds__(kBlock) void k_oneshot(OneshotArgs a, const unsigne
                                                     int rank, unsigned long long seq, int* error) {
     oneshot_chunk(a, send, recv, n, nranks, rank, seq, error, (int)blockIdx.x);
 }
+// ------------------------------------------------------------------ fused exchange
+// Sharded k_step with the one-shot exchange and the list mirror (d.fusedX): the exchange
+// of t runs at the end of k_step(t) itself, so an iteration is one launch per rank and
+// not two (a dependent launch costs 1.5-1.9 us, and k_oneshot's own start ~2.5 us more).
+// Every expanding workgroup calls this at its exit.  Its stores that the exchange reads
+// (R1 deltas: agent atomics; row and block words, R2New bytes: sc1 stores) and its list
+// pushes into the mirrors (system scope) have completed (s_waitcnt vmcnt(0) in every
+// wave, then a barrier); lane 0 adds one to the arrival counter of its shard (block
+// index mod 8: 128 arrivals per counter at 1,024 blocks, below one word's atomic rate,
+// where one counter for all would queue), and the shard's last arrival adds one to the
+// top counter.  The workgroup whose add completes the top counter arrived last: every
+// byte it needs is in memory, and it reads it with sc1 loads (past both caches; per-XCD
+// L2s are not coherent), sends the compact words into the peers' inboxes, raises its
+// flag and waits for theirs (chunk 0 of k_oneshot's flags, the same sequence numbers),
+// and writes recv, which the next launch reads after the kernel boundary.
+constexpr int kFxRegs = 8;   // compact words a thread keeps between its send and its combine
+__device__ __forceinline__ void k_step_exchange(const KgmtDev& d, int nranks, int rank, int nRows, int t) {
+    const int tid = (int)threadIdx.x;
+    __shared__ int sLast;
+    if (tid == 0) {
+        // each counter on a 128-B line of its own (atomics to one line serialise at the memory side)
+        SBMP_GAS unsigned* const arr = G(d.xArrive) + (size_t)(t & 1) * kFxCounters * kFxStride;
+        const int b = (int)blockIdx.x - 1;
+        const int shard = b & 7;
+        const int expect = (nRows - shard + 7) / 8;
+        const unsigned old =
+            __hip_atomic_fetch_add(arr + shard * kFxStride, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        int last = 0;
+        if ((int)old + 1 == expect) {
+            const unsigned top =
+                __hip_atomic_fetch_add(arr + 8 * kFxStride, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            last = ((int)top + 1 == min(8, nRows)) ? 1 : 0;
+        }
+        sLast = last;
+    }
+    __syncthreads();
+    if (!sLast) return;
+    // diagnostics: the worker's stamps in k_oneshot's rows of the timeline (tools/timeline.py --step)
+    long long* const fxTl = (d.timelineFin && t == d.timelineIter && tid == 0) ? d.timelineFin + kTimelineStamps : nullptr;
+    if (fxTl) fxTl[0] = (long long)__builtin_amdgcn_s_memrealtime();
+    const OneshotCompact& x = d.xc;
+    const unsigned long long seq = d.xSeqBase + (unsigned long long)t;
+    const long long n = d.xInboxWords;
+    const size_t par = (size_t)(seq & 1ull) * nranks * n;
+    const size_t flags = (size_t)2 * nranks * n;
+    const unsigned long long* const send = d.stepXs[t & 1];
+    unsigned long long mine[kFxRegs];
+#pragma unroll
+    for (int u = 0; u < kFxRegs; ++u) {
+        const int i = tid + u * kBlock;
+        mine[u] = (i < x.total) ? oneshot_pack<true>(x, send, i, rank, nranks) : 0ull;
+    }
+#pragma unroll
+    for (int u = 0; u < kFxRegs; ++u) {
+        const int i = tid + u * kBlock;
+        if (i < x.total)
+            for (int q = 0; q < nranks; ++q)
+                if (q != rank)
+                    __hip_atomic_store(G(d.xInbox[q]) + par + (size_t)rank * n + i, mine[u], __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+    for (int i = tid + kFxRegs * kBlock; i < x.total; i += kBlock) {   // layouts past kFxRegs words per thread
+        const unsigned long long v = oneshot_pack<true>(x, send, i, rank, nranks);
+        for (int q = 0; q < nranks; ++q)
+            if (q != rank)
+                __hip_atomic_store(d.xInbox[q] + par + (size_t)rank * n + i, v, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+    if (fxTl) fxTl[1] = fxTl[2] = (long long)__builtin_amdgcn_s_memrealtime();
+    if (nranks > 1) {
+        __threadfence_system();   // this thread's stores reach every rank before the flag
+        __syncthreads();
+        if (fxTl) fxTl[3] = (long long)__builtin_amdgcn_s_memrealtime();
+        if (tid < nranks && tid != rank) {   // flag (rank, chunk 0) at peer q; wait for (q, chunk 0) here
+            const int q = tid;
+            __hip_atomic_store(d.xInbox[q] + flags + (size_t)rank * kOneshotChunks, seq, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_SYSTEM);
+            unsigned long long* f = d.xInbox[rank] + flags + (size_t)q * kOneshotChunks;
+            const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
+            while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < seq) {
+                if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > kExchangeWaitTicks) {   // report, do not hang
+                    atomicExch(&d.status->error, kErrExchange);
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(1);
+            }
+        }
+        __threadfence_system();
+        __syncthreads();
+    }
+    if (fxTl) {
+        if (nranks == 1) fxTl[3] = fxTl[2];
+        fxTl[4] = (long long)__builtin_amdgcn_s_memrealtime();
+    }
+    unsigned long long* const recv = const_cast<unsigned long long*>(d.stepXr);
+#pragma unroll
+    for (int u = 0; u < kFxRegs; ++u) {
+        const int i = tid + u * kBlock;
+        if (i < x.total) oneshot_unpack(x, d.xInbox[rank] + par, (size_t)n, recv, i, nranks, rank, mine[u]);
+    }
+    for (int i = tid + kFxRegs * kBlock; i < x.total; i += kBlock)
+        oneshot_unpack(x, d.xInbox[rank] + par, (size_t)n, recv, i, nranks, rank,
+                       oneshot_pack<true>(x, send, i, rank, nranks));
+    if (fxTl) fxTl[5] = (long long)__builtin_amdgcn_s_memrealtime();
+}
+
 size_t oneshot_inbox_words(long long n, int nranks) { return (size_t)2 * nranks * n + (size_t)nranks * kOneshotChunks; }
 
 
@@ -1386,6 +1501,9 @@ __device__ __forceinline__ void step_planner(const KgmtDev& d, const ShardView& 
         if (j * kBlock < nW && w < nW) G(d.R2Avail)[(size_t)cp * nW + w] = snapW[j];
     }
     if constexpr (SH) {   // send parity (t+1) & 1, last read by exchange t-1: zero for k_step(t+1)
+        if (d.fusedX && tid < kFxCounters)   // and the fused exchange's arrival counters of t+1
+            __hip_atomic_store(G(d.xArrive) + ((size_t)((t + 1) & 1) * kFxCounters + tid) * kFxStride, 0u,
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         SBMP_GAS unsigned long long* zx = G(d.stepXs[(t + 1) & 1]);
         for (int i = tid; i < kDeltaReps * d.nR1; i += kBlock) zx[i] = 0ull;
         for (int i = tid; i < d.nR2 / 8; i += kBlock) zx[d.xNewOff + i] = 0ull;   // R2New bytes (count words: owner-written)
@@ -1600,6 +1718,18 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) voi
         __syncthreads();
         q = uniform_plan(sPlan);
     }
+    // the fused exchange's arrival (every exit of an expanding workgroup)
+    auto fx_exit = [&]() {
+        if constexpr (SH) {
+            if (expand && d.fusedX) {
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's stores have completed
+                __syncthreads();
+                k_step_exchange(d, sv.nranks, sv.rank, sv.nRows, t);
+            }
+        }
+    };
+    // the workgroup's work; every exit of it then passes the fused exchange's arrival once
+    auto body = [&]() __attribute__((always_inline)) {
     if (!q.ranPrev) return;
 
     // ---- D6 clear of this block's words of t-1 (KGMT.cu:231,556)
@@ -1920,8 +2050,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) voi
         SBMP_GAS uint8_t* const nb = reinterpret_cast<SBMP_GAS uint8_t*>(G(d.stepXs[cp]) + d.xNewOff);
         for (int i = tid; i < nW; i += kBlock) {
             uint32_t w = sNew[i];
-            while (w) {
-                nb[32 * i + __builtin_ctz(w)] = 1;
+            while (w) {   // written through (sc1): the fused exchange reads them in this launch
+                __hip_atomic_store(nb + 32 * i + __builtin_ctz(w), (uint8_t)1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 w &= w - 1u;
             }
         }
@@ -1942,10 +2072,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) voi
         if (g1 != kNoGoalIdx) gmin = c0 + g1;
         if (g0 != kNoGoalIdx) gmin = g0;
         const int cw = (c0 + c1 + c2 + c3) | ((gmin == kNoGoalIdx ? 0 : gmin + 1) << 16);
-        if constexpr (SH) {   // the block word, and this rank's part of row b (the exchange sums the row)
-            reinterpret_cast<SBMP_GAS int*>(G(d.stepXs[cp]) + d.xCntOff)[gb] = cw;
-            reinterpret_cast<SBMP_GAS int*>(G(d.stepXs[cp]) + d.xRowOff)[b] =
-                (c0 + c1 + c2 + c3) | ((gmin == kNoGoalIdx ? 0 : 1) << 16);
+        if constexpr (SH) {   // the block word, and this rank's part of row b (the exchange sums the row); sc1
+            __hip_atomic_store(reinterpret_cast<SBMP_GAS int*>(G(d.stepXs[cp]) + d.xCntOff) + gb, cw, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(reinterpret_cast<SBMP_GAS int*>(G(d.stepXs[cp]) + d.xRowOff) + b,
+                               (c0 + c1 + c2 + c3) | ((gmin == kNoGoalIdx ? 0 : 1) << 16), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
         }
         else G(d.stepCnt)[(size_t)cp * kMaxStepBlocks + b] = cw;
     }
@@ -1958,6 +2090,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) voi
     }
     if (tl && lane == 0)
         for (int i = 0; i < kTimelineStamps; ++i) G(tl)[i] = stamp[i];
+    };
+    body();
+    fx_exit();
 #undef SBMP_STAMP
 }
 
@@ -2245,6 +2380,23 @@ void launch_fold_r2(const KgmtDev& d, int tFirst, int tLast, hipStream_t s, cons
     launch(k_fold_r2, grid, dim3(1024), shm, s, tm, d, tFirst);
 }
 
+OneshotCompact oneshot_compact(const OneshotLayout& l) {
+    OneshotCompact x{};
+    x.nR1 = l.nR1;
+    x.rowOff = l.rowOff;
+    x.rowWords = (l.rows + 1) / 2;
+    x.cntOff = l.cntOff;
+    x.owned = l.owned;
+    x.nBlocks = l.nBlocks;
+    x.newOff = l.newOff;
+    x.newWords = l.newWords;
+    x.cR = x.nR1;
+    x.cB = x.cR + x.rowWords;
+    x.cN = x.cB + (x.owned + 1) / 2;
+    x.total = x.cN + (x.newWords + 7) / 8;
+    return x;
+}
+
 void launch_oneshot(unsigned long long* const* inbox, const unsigned long long* send, unsigned long long* recv,
                     long long n, int nranks, int rank, unsigned long long seq, int* error, hipStream_t s,
                     const KernelTiming& tm, const OneshotLayout* compact,
@@ -2252,21 +2404,8 @@ void launch_oneshot(unsigned long long* const* inbox, const unsigned long long* 
     OneshotArgs a{};
     for (int q = 0; q < nranks; ++q) a.inbox[q] = inbox[q];
     if (compact && compact->on) {
-        OneshotCompact& x = a.cx;
-        a.compactOn = 1;
-        x.nR1 = compact->nR1;
-        x.rowOff = compact->rowOff;
-        x.rowWords = (compact->rows + 1) / 2;
-        x.cntOff = compact->cntOff;
-        x.owned = compact->owned;
-        x.nBlocks = compact->nBlocks;
-        x.newOff = compact->newOff;
-        x.newWords = compact->newWords;
-        x.cR = x.nR1;
-        x.cB = x.cR + x.rowWords;
-        x.cN = x.cB + (x.owned + 1) / 2;
-        x.total = x.cN + (x.newWords + 7) / 8;
-        if (x.total > n) a.compactOn = 0;   // cannot happen (the compact form is smaller); the full sum is exact too
+        a.cx = oneshot_compact(*compact);
+        a.compactOn = (a.cx.total <= n) ? 1 : 0;   // always (the compact form is smaller); the full sum is exact too
     }
     a.tl = tl;
     launch(k_oneshot, dim3(kOneshotChunks), dim3(kBlock), 0, s, tm, a, send, recv, n, nranks, rank, seq, error);

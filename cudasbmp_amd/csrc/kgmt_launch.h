@@ -53,6 +53,7 @@ struct OneshotLayout {
     int cntOff, owned, nBlocks;   // u64 offset of the block words (ints), owned blocks, global blocks
     int newOff, newWords;     // u64 offset and words of the R2New bytes
 };
+OneshotCompact oneshot_compact(const OneshotLayout& l);   // the compact layout of l
 // tl: diagnostics, 8 stamps per workgroup, or null.
 void launch_oneshot(unsigned long long* const* inbox, const unsigned long long* send, unsigned long long* recv,
                     long long n, int nranks, int rank, unsigned long long seq, int* error, hipStream_t s,

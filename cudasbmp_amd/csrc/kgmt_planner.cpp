@@ -353,6 +353,31 @@ KgmtPlanner::KgmtPlanner(const sbmp_kgmt_params& p, int nranks, int rank, Exchan
             d.stepMirror = own;
             d.listPlain = 1;
         }
+        // The fused exchange (k_step_exchange, kgmt_kernels.hip): with the mirror and the
+        // compact form, the last expanding workgroup of k_step runs the exchange, and no
+        // k_oneshot is launched.  Opt-in (SBMP_FUSED_EXCHANGE=1; DESIGN.md §7 has the
+        // measurements).  The same on every rank: it depends on the all-reduced one-shot
+        // verdict and the switches.
+        const char* fv = getenv("SBMP_FUSED_EXCHANGE");
+        if (d.stepMirror && compactX_ && fv && atoi(fv) == 1) {
+            d.fusedX = 1;
+            for (int q = 0; q < nranks; ++q) d.xInbox[q] = inbox_[q];
+            d.xInboxWords = (int)xWords_;
+            d.xArrive = alloc<unsigned>((size_t)2 * kFxCounters * kFxStride);
+            SBMP_HIP(hipMemset(d.xArrive, 0, sizeof(unsigned) * 2 * kFxCounters * kFxStride));
+            OneshotLayout l{};
+            l.on = 1;
+            l.nR1 = d.nR1;
+            l.rowOff = d.xRowOff;
+            l.rows = expandBlocks_;
+            l.cntOff = d.xCntOff;
+            l.owned = expandBlocks_;
+            l.nBlocks = d.nBlocks;
+            l.newOff = d.xNewOff;
+            l.newWords = (int)xWords_ - d.xNewOff;
+            d.xc = oneshot_compact(l);
+            if (d.xc.total > (int)xWords_) d.fusedX = 0;   // cannot happen (compact is smaller)
+        }
     }
 }
 
@@ -442,6 +467,10 @@ void KgmtPlanner::begin(const float* initial, const float* goal, const float* d_
     if (xSendOdd_ != xSend_) SBMP_HIP(hipMemsetAsync(xSendOdd_, 0, sizeof(unsigned long long) * xWords_, s));
     if (local_) SBMP_HIP(hipMemsetAsync(local_, 0, sizeof(unsigned long long) * localWords_, s));
     if (xRecv_ != xSend_) SBMP_HIP(hipMemsetAsync(xRecv_, 0, sizeof(unsigned long long) * xWords_, s));
+    if (d.fusedX) {   // exchange t of this plan has sequence number xSeqBase + t
+        SBMP_HIP(hipMemsetAsync(d.xArrive, 0, sizeof(unsigned) * 2 * kFxCounters * kFxStride, s));
+        d.xSeqBase = xSeq_;
+    }
     SBMP_HIP(hipMemsetAsync(d.R1, 0, sizeof(int) * 2 * 5 * d.nR1, s));   // both parities
     SBMP_HIP(hipMemsetAsync(d.R2Avail, 0, sizeof(uint32_t) * 2 * (d.nR2 / 32), s));
     if (stepCapable_) SBMP_HIP(hipMemsetAsync(d.stepPub, 0, sizeof(unsigned long long) * 2 * (d.nR1 + d.nR2 / 32), s));
@@ -566,6 +595,7 @@ void KgmtPlanner::path_info(sbmp_path_info* out) {
     out->rank = d.rank;
     out->commRanks = ex_ ? ex_->comm_ranks() : 0;
     out->listMirror = d.stepMirror ? 1 : 0;
+    out->fusedExchange = d.fusedX ? 1 : 0;
 }
 
 void KgmtPlanner::build_grid(const float* d_obstacles, int nObs) {
@@ -646,6 +676,13 @@ void KgmtPlanner::stage_step(int t) {
 
 void KgmtPlanner::stage_exchange(int t) {
     if (!ex_) return;
+    if (d_.fusedX) {   // k_step(t) ran the exchange itself
+        ++xSeq_;
+        if (xSeq_ != d_.xSeqBase + (unsigned long long)t)
+            throw Error(SBMP_ERR_STATE, "fused exchange: sequence " + std::to_string(xSeq_) + " at iteration " +
+                                            std::to_string(t));
+        return;
+    }
     const unsigned long long* send = exchange_send(t);
     if (oneshot_) {
         ++xSeq_;

@@ -333,7 +333,7 @@ class KGMT:
                 "resident_groups": pi.residentGroups, "needed_groups": pi.neededGroups,
                 "exchange": self.EXCHANGES[pi.exchange] if 0 <= pi.exchange < 3 else pi.exchange,
                 "nranks": pi.nranks, "rank": pi.rank, "rccl_nranks": pi.commRanks,
-                "list_mirror": bool(pi.listMirror)}
+                "list_mirror": bool(pi.listMirror), "fused_exchange": bool(pi.fusedExchange)}
 
     def kernel_samples(self, name: str) -> np.ndarray:
         """Per-launch durations (ms) of kernel `name` since the last reset_kernel_stats()."""

@@ -114,6 +114,8 @@ typedef struct sbmp_path_info {
     int commRanks;            /* ranks of the RCCL communicator (0: none) */
     int listMirror;           /* 1: the one-shot exchange copies the flagged-children lists into each
                                  rank's mirror, and k_step reads its parents from local HBM */
+    int fusedExchange;        /* 1: the last expanding workgroup of k_step runs the one-shot exchange
+                                 (no k_oneshot launch) */
 } sbmp_path_info;
 
 typedef struct sbmp_kgmt sbmp_kgmt;

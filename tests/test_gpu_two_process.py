@@ -9,7 +9,9 @@ every rank's IPC-mapped inbox and raises flags; both processes' kernels meet on 
 GPU; the inboxes are uncached device memory) as its own k_oneshot launch, or, with
 SBMP_EXCHANGE=collective, by the Exchange's all-reduce.  With the one-shot exchange the
 same kernel also pushes each rank's lists into every rank's list mirror, and k_step reads
-its parents from its own memory (SBMP_MIRROR=0: from the peer's record buffer).
+its parents from its own memory (SBMP_MIRROR=0: from the peer's record buffer); by
+request (SBMP_FUSED_EXCHANGE=1) the exchange itself runs in k_step's tail, done by its
+last expanding workgroup, with no k_oneshot launch.
 RCCL cannot put two ranks on one device, so that all-reduce and the IPC handle
 exchange run over torch.distributed gloo through the host-collectives seam
 (cudasbmp_amd/host_comm.py).  The ranks' merged state must equal the CPU oracle's
@@ -47,6 +49,10 @@ def _rank_main(rank, port, kw, seed, out_dir, exchange, delay=0.0):
         os.environ["SBMP_MIRROR"] = "0"
     else:
         os.environ.pop("SBMP_MIRROR", None)
+    if exchange == "oneshot-fused":   # the exchange in k_step's tail instead of its own k_oneshot launch
+        os.environ["SBMP_FUSED_EXCHANGE"] = "1"
+    else:
+        os.environ.pop("SBMP_FUSED_EXCHANGE", None)
     if exchange == "oneshot-check-fails" and rank == 1:   # only rank 1's start-up check "fails"
         os.environ["SBMP_ONESHOT_SELFTEST"] = "fail"
     else:
@@ -68,14 +74,15 @@ def _rank_main(rank, port, kw, seed, out_dir, exchange, delay=0.0):
     g.set_profiling(True)   # counts the launches: which exchange ran
     r = g.plan(DEMO_INITIAL, DEMO_GOAL, DeviceBuffer(obs), len(obs), seed=seed)
     oneshots = g.kernel_stats().get("k_oneshot", (0, 0.0))[0]
-    mirror = g.path_info()["list_mirror"]
+    pinfo = g.path_info()
+    mirror, fused = pinfo["list_mirror"], pinfo["fused_exchange"]
     s, p, c = g.tree()
     G, GN = g.flags()          # GNew words live with their owner: merged by the all-reduce
     reg = g.regions()          # R2Valid / R2Invalid: each rank folded its own children
     u, up = g.unexplored()     # slots of other ranks read as 0 / -1
     rng = g.rng()
     np.savez(os.path.join(out_dir, f"rank{rank}.npz"), s=s, p=p, c=c, G=G, GN=GN, u=u, up=up, rng=rng,
-             log=g.iter_log(), res=np.array([r.iterations, r.treeSize, r.goalIndex]), oneshots=oneshots, mirror=mirror,
+             log=g.iter_log(), res=np.array([r.iterations, r.treeSize, r.goalIndex]), oneshots=oneshots, mirror=mirror, fused=fused,
              cost=np.float32(r.costToGoal), **{"reg_" + k: v for k, v in reg.items()})
     g.close()
     dist.destroy_process_group()
@@ -91,6 +98,9 @@ def _rank_main(rank, port, kw, seed, out_dir, exchange, delay=0.0):
      "collective", 0.0),
     (dict(samplesPerIteration=4096, batchRule="fill", maxTreeSize=200000, numIterations=15, goalThreshold=0.0), 21,
      "oneshot-remote", 0.0),
+    (dict(samplesPerIteration=4096, batchRule="fill", maxTreeSize=200000, numIterations=15, goalThreshold=0.0), 21,
+     "oneshot-fused", 0.0),
+    (dict(fixGNewClear=True, numIterations=40), 8, "oneshot-fused", 0.0),
     # rank 1 starts 3 s late (round 2's exchange gave up after 1 s)
     (dict(samplesPerIteration=4096, batchRule="fill", maxTreeSize=200000, numIterations=15, goalThreshold=0.0), 21,
      "oneshot", 3.0),
@@ -128,12 +138,17 @@ def test_two_processes_one_gpu_bit_exact(kw, seed, exchange, delay, tmp_path, ob
     n = o.rng().shape[0]
     owner = (np.arange(n) // 256) % WORLD
     for r, d in enumerate(R):
-        if exchange.startswith("oneshot") and exchange != "oneshot-check-fails":
+        # default: the lists go into every rank's mirror and k_oneshot exchanges the counters;
+        # SBMP_FUSED_EXCHANGE=1 runs the exchange in k_step's tail (no k_oneshot launch);
+        # SBMP_MIRROR=0 reads the lists over the mapping; the collective exchange uses neither
+        fused = exchange == "oneshot-fused"
+        assert bool(d["fused"]) == fused, f"rank {r}: fused exchange {bool(d['fused'])}"
+        assert bool(d["mirror"]) == (exchange in ("oneshot", "oneshot-fused", "oneshot-kernel")), \
+            f"rank {r}: list mirror {bool(d['mirror'])}"
+        if exchange in ("oneshot", "oneshot-remote"):
             assert int(d["oneshots"]) > 0, f"rank {r}: the one-shot exchange did not run"
         else:
             assert int(d["oneshots"]) == 0, f"rank {r}: k_oneshot ran ({int(d['oneshots'])} launches)"
-        # the one-shot exchange pushes the lists into each rank's mirror (SBMP_MIRROR=0: remote reads)
-        assert bool(d["mirror"]) == (exchange == "oneshot"), f"rank {r}: list mirror {bool(d['mirror'])}"
     for r, d in enumerate(R):   # every rank holds the whole tree and the merged exports
         assert np.array_equal(d["log"], o.iter_logs()), f"rank {r}: iteration logs differ"
         assert np.array_equal(d["p"], po), f"rank {r}: parents differ"
