@@ -976,36 +976,47 @@ __global__ __launch_bounds__(kBlock) void k_oneshot(OneshotArgs a, const unsigne
 // pushes into the mirrors (system scope) have completed (s_waitcnt vmcnt(0) in every
 // wave, then a barrier); lane 0 adds one to the arrival counter of its shard (block
 // index mod 8: 128 arrivals per counter at 1,024 blocks, below one word's atomic rate,
-// where one counter for all would queue), and the shard's last arrival adds one to the
-// top counter.  The workgroup whose add completes the top counter arrived last: every
-// byte it needs is in memory, and it reads it with sc1 loads (past both caches; per-XCD
-// L2s are not coherent), sends the compact words into the peers' inboxes, raises its
-// flag and waits for theirs (chunk 0 of k_oneshot's flags, the same sequence numbers),
-// and writes recv, which the next launch reads after the kernel boundary.
-constexpr int kFxRegs = 8;   // compact words a thread keeps between its send and its combine
+// where one counter for all would queue; each counter on a line of its own), and the
+// shard's last arrival adds one to the top counter and waits until every shard is in.
+// Those eight workgroups are then the workers: every byte they need is in memory, and
+// worker c reads chunk c of the compact words with sc1 loads (past both caches; per-XCD
+// L2s are not coherent), sends it into the peers' inboxes, raises its flag and waits for
+// theirs (chunk c of k_oneshot's flags, the same sequence numbers), and writes its part
+// of recv, which the next launch reads after the kernel boundary.
+constexpr int kFxRegs = 4;   // compact words a thread keeps between its send and its combine
 __device__ __forceinline__ void k_step_exchange(const KgmtDev& d, int nranks, int rank, int nRows, int t) {
     const int tid = (int)threadIdx.x;
-    __shared__ int sLast;
+    const int nW = min(8, nRows);   // workers: the last arrival of each shard
+    __shared__ int sRole;
+    // each counter on a 128-B line of its own (atomics to one line serialise at the memory side)
+    SBMP_GAS unsigned* const arr = G(d.xArrive) + (size_t)(t & 1) * kFxCounters * kFxStride;
     if (tid == 0) {
-        // each counter on a 128-B line of its own (atomics to one line serialise at the memory side)
-        SBMP_GAS unsigned* const arr = G(d.xArrive) + (size_t)(t & 1) * kFxCounters * kFxStride;
         const int b = (int)blockIdx.x - 1;
         const int shard = b & 7;
         const int expect = (nRows - shard + 7) / 8;
         const unsigned old =
             __hip_atomic_fetch_add(arr + shard * kFxStride, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        int last = 0;
-        if ((int)old + 1 == expect) {
-            const unsigned top =
-                __hip_atomic_fetch_add(arr + 8 * kFxStride, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            last = ((int)top + 1 == min(8, nRows)) ? 1 : 0;
+        int role = -1;
+        if ((int)old + 1 == expect) {   // the shard's last arrival: worker `shard`, once every shard is in
+            __hip_atomic_fetch_add(arr + 8 * kFxStride, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
+            while ((int)__hip_atomic_load(arr + 8 * kFxStride, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < nW) {
+                if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > kExchangeWaitTicks) {   // report, do not hang
+                    atomicExch(&d.status->error, kErrExchange);
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(1);
+            }
+            role = shard;
         }
-        sLast = last;
+        sRole = role;
     }
     __syncthreads();
-    if (!sLast) return;
-    // diagnostics: the worker's stamps in k_oneshot's rows of the timeline (tools/timeline.py --step)
-    long long* const fxTl = (d.timelineFin && t == d.timelineIter && tid == 0) ? d.timelineFin + kTimelineStamps : nullptr;
+    const int c = sRole;
+    if (c < 0) return;
+    // diagnostics: worker 0's stamps in k_oneshot's rows of the timeline (tools/timeline.py --step)
+    long long* const fxTl =
+        (d.timelineFin && t == d.timelineIter && tid == 0) ? d.timelineFin + (size_t)(1 + c) * kTimelineStamps : nullptr;
     if (fxTl) fxTl[0] = (long long)__builtin_amdgcn_s_memrealtime();
     const OneshotCompact& x = d.xc;
     const unsigned long long seq = d.xSeqBase + (unsigned long long)t;
@@ -1013,38 +1024,40 @@ __device__ __forceinline__ void k_step_exchange(const KgmtDev& d, int nranks, in
     const size_t par = (size_t)(seq & 1ull) * nranks * n;
     const size_t flags = (size_t)2 * nranks * n;
     const unsigned long long* const send = d.stepXs[t & 1];
+    const int per = (x.total + nW - 1) / nW;
+    const int lo = c * per, hi = min(x.total, lo + per);
     unsigned long long mine[kFxRegs];
 #pragma unroll
     for (int u = 0; u < kFxRegs; ++u) {
-        const int i = tid + u * kBlock;
-        mine[u] = (i < x.total) ? oneshot_pack<true>(x, send, i, rank, nranks) : 0ull;
+        const int i = lo + tid + u * kBlock;
+        mine[u] = (i < hi) ? oneshot_pack<true>(x, send, i, rank, nranks) : 0ull;
     }
 #pragma unroll
     for (int u = 0; u < kFxRegs; ++u) {
-        const int i = tid + u * kBlock;
-        if (i < x.total)
+        const int i = lo + tid + u * kBlock;
+        if (i < hi)
             for (int q = 0; q < nranks; ++q)
                 if (q != rank)
                     __hip_atomic_store(G(d.xInbox[q]) + par + (size_t)rank * n + i, mine[u], __ATOMIC_RELAXED,
                                        __HIP_MEMORY_SCOPE_SYSTEM);
     }
-    for (int i = tid + kFxRegs * kBlock; i < x.total; i += kBlock) {   // layouts past kFxRegs words per thread
+    for (int i = lo + tid + kFxRegs * kBlock; i < hi; i += kBlock) {   // chunks past kFxRegs words per thread
         const unsigned long long v = oneshot_pack<true>(x, send, i, rank, nranks);
         for (int q = 0; q < nranks; ++q)
             if (q != rank)
-                __hip_atomic_store(d.xInbox[q] + par + (size_t)rank * n + i, v, __ATOMIC_RELAXED,
+                __hip_atomic_store(G(d.xInbox[q]) + par + (size_t)rank * n + i, v, __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_SYSTEM);
     }
-    if (fxTl) fxTl[1] = fxTl[2] = (long long)__builtin_amdgcn_s_memrealtime();
+    if (fxTl) fxTl[1] = fxTl[2] = fxTl[3] = (long long)__builtin_amdgcn_s_memrealtime();
     if (nranks > 1) {
         __threadfence_system();   // this thread's stores reach every rank before the flag
         __syncthreads();
         if (fxTl) fxTl[3] = (long long)__builtin_amdgcn_s_memrealtime();
-        if (tid < nranks && tid != rank) {   // flag (rank, chunk 0) at peer q; wait for (q, chunk 0) here
+        if (tid < nranks && tid != rank) {   // flag (rank, chunk c) at peer q; wait for (q, chunk c) here
             const int q = tid;
-            __hip_atomic_store(d.xInbox[q] + flags + (size_t)rank * kOneshotChunks, seq, __ATOMIC_RELAXED,
+            __hip_atomic_store(d.xInbox[q] + flags + (size_t)rank * kOneshotChunks + c, seq, __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_SYSTEM);
-            unsigned long long* f = d.xInbox[rank] + flags + (size_t)q * kOneshotChunks;
+            unsigned long long* f = d.xInbox[rank] + flags + (size_t)q * kOneshotChunks + c;
             const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
             while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < seq) {
                 if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > kExchangeWaitTicks) {   // report, do not hang
@@ -1057,17 +1070,14 @@ __device__ __forceinline__ void k_step_exchange(const KgmtDev& d, int nranks, in
         __threadfence_system();
         __syncthreads();
     }
-    if (fxTl) {
-        if (nranks == 1) fxTl[3] = fxTl[2];
-        fxTl[4] = (long long)__builtin_amdgcn_s_memrealtime();
-    }
+    if (fxTl) fxTl[4] = (long long)__builtin_amdgcn_s_memrealtime();
     unsigned long long* const recv = const_cast<unsigned long long*>(d.stepXr);
 #pragma unroll
     for (int u = 0; u < kFxRegs; ++u) {
-        const int i = tid + u * kBlock;
-        if (i < x.total) oneshot_unpack(x, d.xInbox[rank] + par, (size_t)n, recv, i, nranks, rank, mine[u]);
+        const int i = lo + tid + u * kBlock;
+        if (i < hi) oneshot_unpack(x, d.xInbox[rank] + par, (size_t)n, recv, i, nranks, rank, mine[u]);
     }
-    for (int i = tid + kFxRegs * kBlock; i < x.total; i += kBlock)
+    for (int i = lo + tid + kFxRegs * kBlock; i < hi; i += kBlock)
         oneshot_unpack(x, d.xInbox[rank] + par, (size_t)n, recv, i, nranks, rank,
                        oneshot_pack<true>(x, send, i, rank, nranks));
     if (fxTl) fxTl[5] = (long long)__builtin_amdgcn_s_memrealtime();

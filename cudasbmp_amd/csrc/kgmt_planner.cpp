@@ -355,11 +355,11 @@ KgmtPlanner::KgmtPlanner(const sbmp_kgmt_params& p, int nranks, int rank, Exchan
         }
         // The fused exchange (k_step_exchange, kgmt_kernels.hip): with the mirror and the
         // compact form, the last expanding workgroup of k_step runs the exchange, and no
-        // k_oneshot is launched.  Opt-in (SBMP_FUSED_EXCHANGE=1; DESIGN.md §7 has the
-        // measurements).  The same on every rank: it depends on the all-reduced one-shot
-        // verdict and the switches.
+        // k_oneshot is launched (SBMP_FUSED_EXCHANGE=0: the separate kernel; DESIGN.md §7
+        // has the measurements).  The same on every rank: it depends on the all-reduced
+        // one-shot verdict and the switches.
         const char* fv = getenv("SBMP_FUSED_EXCHANGE");
-        if (d.stepMirror && compactX_ && fv && atoi(fv) == 1) {
+        if (d.stepMirror && compactX_ && !(fv && atoi(fv) == 0)) {
             d.fusedX = 1;
             for (int q = 0; q < nranks; ++q) d.xInbox[q] = inbox_[q];
             d.xInboxWords = (int)xWords_;

@@ -10,8 +10,8 @@ GPU; the inboxes are uncached device memory) as its own k_oneshot launch, or, wi
 SBMP_EXCHANGE=collective, by the Exchange's all-reduce.  With the one-shot exchange the
 same kernel also pushes each rank's lists into every rank's list mirror, and k_step reads
 its parents from its own memory (SBMP_MIRROR=0: from the peer's record buffer); by
-request (SBMP_FUSED_EXCHANGE=1) the exchange itself runs in k_step's tail, done by its
-last expanding workgroup, with no k_oneshot launch.
+default the exchange itself then runs in k_step's tail, done by the last arrivals of its
+expanding workgroups, with no k_oneshot launch (SBMP_FUSED_EXCHANGE=0: the separate kernel).
 RCCL cannot put two ranks on one device, so that all-reduce and the IPC handle
 exchange run over torch.distributed gloo through the host-collectives seam
 (cudasbmp_amd/host_comm.py).  The ranks' merged state must equal the CPU oracle's
@@ -49,8 +49,8 @@ def _rank_main(rank, port, kw, seed, out_dir, exchange, delay=0.0):
         os.environ["SBMP_MIRROR"] = "0"
     else:
         os.environ.pop("SBMP_MIRROR", None)
-    if exchange == "oneshot-fused":   # the exchange in k_step's tail instead of its own k_oneshot launch
-        os.environ["SBMP_FUSED_EXCHANGE"] = "1"
+    if exchange == "oneshot-kernel":   # the exchange as its own k_oneshot launch, not in k_step's tail
+        os.environ["SBMP_FUSED_EXCHANGE"] = "0"
     else:
         os.environ.pop("SBMP_FUSED_EXCHANGE", None)
     if exchange == "oneshot-check-fails" and rank == 1:   # only rank 1's start-up check "fails"
@@ -99,8 +99,8 @@ def _rank_main(rank, port, kw, seed, out_dir, exchange, delay=0.0):
     (dict(samplesPerIteration=4096, batchRule="fill", maxTreeSize=200000, numIterations=15, goalThreshold=0.0), 21,
      "oneshot-remote", 0.0),
     (dict(samplesPerIteration=4096, batchRule="fill", maxTreeSize=200000, numIterations=15, goalThreshold=0.0), 21,
-     "oneshot-fused", 0.0),
-    (dict(fixGNewClear=True, numIterations=40), 8, "oneshot-fused", 0.0),
+     "oneshot-kernel", 0.0),
+    (dict(fixGNewClear=True, numIterations=40), 8, "oneshot-kernel", 0.0),
     # rank 1 starts 3 s late (round 2's exchange gave up after 1 s)
     (dict(samplesPerIteration=4096, batchRule="fill", maxTreeSize=200000, numIterations=15, goalThreshold=0.0), 21,
      "oneshot", 3.0),
@@ -138,14 +138,14 @@ def test_two_processes_one_gpu_bit_exact(kw, seed, exchange, delay, tmp_path, ob
     n = o.rng().shape[0]
     owner = (np.arange(n) // 256) % WORLD
     for r, d in enumerate(R):
-        # default: the lists go into every rank's mirror and k_oneshot exchanges the counters;
-        # SBMP_FUSED_EXCHANGE=1 runs the exchange in k_step's tail (no k_oneshot launch);
-        # SBMP_MIRROR=0 reads the lists over the mapping; the collective exchange uses neither
-        fused = exchange == "oneshot-fused"
+        # default: the lists go into every rank's mirror and the exchange runs in k_step's tail
+        # (no k_oneshot launch); SBMP_FUSED_EXCHANGE=0 launches k_oneshot; SBMP_MIRROR=0 reads the
+        # lists over the mapping, with k_oneshot; the collective exchange uses neither
+        fused = exchange == "oneshot"
         assert bool(d["fused"]) == fused, f"rank {r}: fused exchange {bool(d['fused'])}"
-        assert bool(d["mirror"]) == (exchange in ("oneshot", "oneshot-fused", "oneshot-kernel")), \
+        assert bool(d["mirror"]) == (exchange in ("oneshot", "oneshot-kernel")), \
             f"rank {r}: list mirror {bool(d['mirror'])}"
-        if exchange in ("oneshot", "oneshot-remote"):
+        if exchange in ("oneshot-kernel", "oneshot-remote"):
             assert int(d["oneshots"]) > 0, f"rank {r}: the one-shot exchange did not run"
         else:
             assert int(d["oneshots"]) == 0, f"rank {r}: k_oneshot ran ({int(d['oneshots'])} launches)"

@@ -14,6 +14,9 @@
 #   tools/gpu_cycle.sh bench <out> <name> [args]   one bench line into <out>/<name>.json
 #   tools/gpu_cycle.sh shard <out>                 tools/shard_cost.py 1 2 8 and two ranks on one GPU
 #   tools/gpu_cycle.sh microbench <out>            build and run tools/microbench/{valu,salu}_bench
+#   tools/gpu_cycle.sh final <out>                 the round's record: pytest -m gpu, the default bench line,
+#                                                  two driver-form lines, a 300-step line, the rocprofv3
+#                                                  kernel-trace summary of the default line, c5 at 131,072
 #
 # Several steps in one call:  tools/gpu_cycle.sh tests o && tools/gpu_cycle.sh ab o 2 prev=_ab/prev new=.
 set -uo pipefail
@@ -77,6 +80,27 @@ shard)
     timeout -k 10 300 python3 bench.py --gpus 2 --collectives host --steps 50 --warmup 10 --no-cpu-baseline --no-ttfs \
         > "$R/$out/bench_2rank_host.json" 2> "$R/$out/bench_2rank_host.err" || { tail -5 "$R/$out/bench_2rank_host.err"; exit 1; }
     tail -1 "$R/$out/bench_2rank_host.json" ;;
+final)
+    timeout -k 10 900 python3 -u -m pytest tests -x -q -m gpu --timeout 180 --timeout-method thread \
+        -p no:cacheprovider > "$R/$out/gpu_tests.log" 2>&1 || { tail -20 "$R/$out/gpu_tests.log"; exit 1; }
+    tail -1 "$R/$out/gpu_tests.log"
+    timeout -k 10 300 python3 bench.py > "$R/$out/bench.json" 2> "$R/$out/bench.err" || { tail -5 "$R/$out/bench.err"; exit 1; }
+    line "$R/$out/bench.json" default
+    for rep in 1 2; do
+        timeout -k 10 200 python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-ttfs > "$R/$out/drv_$rep.json" \
+            2> "$R/$out/drv_$rep.err" || exit 1
+        line "$R/$out/drv_$rep.json" "driver $rep"
+    done
+    timeout -k 10 200 python3 bench.py --steps 300 --warmup 20 --no-cpu-baseline --no-ttfs > "$R/$out/s300.json" \
+        2> "$R/$out/s300.err" || exit 1
+    line "$R/$out/s300.json" s300
+    timeout -k 10 300 python3 bench.py --workload c5 --samples-per-gpu 131072 --no-cpu-baseline --no-ttfs \
+        > "$R/$out/c5_131k.json" 2> "$R/$out/c5_131k.err" || exit 1
+    line "$R/$out/c5_131k.json" c5_131k
+    cd /tmp && export TMPDIR=/tmp
+    timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$R/$out/trace" -o run --output-format csv -- \
+        python3 "$R/bench.py" --no-cpu-baseline > "$R/$out/bench_traced.json" 2> "$R/$out/bench_traced.err" || exit 1
+    cd "$R" && line "$out/bench_traced.json" traced ;;
 microbench)
     for b in valu_bench salu_bench; do
         /opt/rocm/bin/hipcc -O3 --offload-arch=gfx950 "tools/microbench/$b.hip" -o "/tmp/$b" || exit 1
