@@ -55,7 +55,7 @@ def main():
         ex = f[8:8 + 64].reshape(8, 8)   # k_oneshot of the same iteration (sharded ranks), one row per chunk
         if (ex[:, 0] != 0).any():
             t_end = a[a[:, 6] != 0, 6].max()
-            print("k_oneshot chunks (us after the last k_step wave's end):  entry  stored  mirror  fenced  "
+            print("exchange (k_oneshot chunks, or the fused workers; us after the last k_step wave's end):  entry  stored  mirror  fenced  "
                   "flags   end")
             for c in range(8):
                 if ex[c, 0]:
