@@ -1604,12 +1604,16 @@ __device__ __forceinline__ void step_planner(const KgmtDev& d, const ShardView& 
 //   ctrlPrev ctrl[t-1]
 template <int AGENT, int OBS, bool SH>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) void k_step(
-    const KgmtDev* __restrict__ dp, int t, int expand, const int4* __restrict__ cnt4,
+    const KgmtDev* __restrict__ dp, int tx, int shRR, const int4* __restrict__ cnt4,
     const IterCtrl* __restrict__ ctrlPrev, const uint4* __restrict__ rngAArg, const uint2* __restrict__ rngBArg,
     const unsigned long long* __restrict__ gnewArg, const PlannerStatus* __restrict__ statusArg, long long* tlBase,
-    int shRanks, int shRank, int shRows, const int* __restrict__ shBw) {
+    int shRows, const int* __restrict__ shBw) {
+    // tx = t | expand << 31 and shRR = rank | ranks << 8 share the preloaded argument
+    // dwords with the prologue's first pointers (a sharded slot index needs the rank
+    // before its first load)
+    const int t = tx & 0x7fffffff, expand = (int)((unsigned)tx >> 31);
     const KgmtDev& d = *dp;
-    const ShardView sv{SH ? shRanks : 1, SH ? shRank : 0, SH ? shRows : 0, G(shBw)};
+    const ShardView sv{SH ? (shRR >> 8) : 1, SH ? (shRR & 0xff) : 0, SH ? shRows : 0, G(shBw)};
     extern __shared__ float4 sDyn[];   // [LDS obstacles][prefix: nBlocks + 1 ints][R2New bits: nR2 / 32]
     __shared__ int sR1P[kMaxR1];
     __shared__ StepPlan sPlan;
@@ -2289,9 +2293,9 @@ static void launch_step_form(const KgmtDev& d, int t, int expand, int variant, h
     long long* const tlBase = (d.timeline && t == d.timelineIter && expand) ? d.timeline : nullptr;
     const int4* const cnt4 = SH ? reinterpret_cast<const int4*>(d.stepXr + d.xRowOff)
                                 : reinterpret_cast<const int4*>(d.stepCnt + (size_t)((t - 1) & 1) * kMaxStepBlocks);
-#define SBMP_STEP_ARGS                                                                                      \
-    d.devSelf, t, expand, cnt4, d.ctrl + (t - 1), d.rngA, d.rngB, d.gnewOut, d.status, tlBase, SH ? d.nranks : 1, \
-        SH ? d.rank : 0, SH ? d.nBlocks / d.nranks : d.nBlocks,                                                   \
+#define SBMP_STEP_ARGS                                                                                        \
+    d.devSelf, (int)((unsigned)t | ((unsigned)(expand != 0) << 31)), SH ? (d.rank | (d.nranks << 8)) : (1 << 8),  \
+        cnt4, d.ctrl + (t - 1), d.rngA, d.rngB, d.gnewOut, d.status, tlBase, SH ? d.nBlocks / d.nranks : d.nBlocks, \
         SH ? reinterpret_cast<const int*>(d.stepXr + d.xCntOff) : nullptr
     if (d.gridStart) {
         launch(k_step<AGENT, kObsGrid, SH>, grid, block, pfx, s, tm, SBMP_STEP_ARGS);
@@ -2320,7 +2324,7 @@ static void launch_step_form(const KgmtDev& d, int t, int expand, int variant, h
 // The k_step instantiation launch_step_form picks, and its dynamic LDS, for the
 // residency check (step_resident_groups).
 using StepFn = void (*)(const KgmtDev*, int, int, const int4*, const IterCtrl*, const uint4*, const uint2*,
-                        const unsigned long long*, const PlannerStatus*, long long*, int, int, int, const int*);
+                        const unsigned long long*, const PlannerStatus*, long long*, int, const int*);
 template <int AGENT, bool SH>
 static StepFn step_fn(const KgmtDev& d, int variant, size_t* shm) {
     const size_t nS = SH ? d.nBlocks / d.nranks : d.nBlocks;
