@@ -641,8 +641,12 @@ struct GridRun {
     int b0, e0, b1, e1;   // runs of rows cy0 and cy0 + 1 (e1 = b1 for a one-row span)
 };
 
-__device__ __forceinline__ GridRun grid_run(float minx, float miny, float maxx, float maxy, const KgmtDev& d) {
-    const SBMP_GAS int* const start = G(d.gridStart);
+// The cell-start table: in global memory (G(d.gridStart)), or staged in LDS by k_step
+// (SP = const SBMP_LDS int*, one LDS read per row lookup instead of an L2 round trip).
+#define SBMP_LDS __attribute__((address_space(3)))
+template <class SP>
+__device__ __forceinline__ GridRun grid_run(float minx, float miny, float maxx, float maxy, const KgmtDev& d,
+                                            SP start) {
     const int g = d.gridG;
     const float top = (float)(g - 1);
     auto cell = [&](float v, float inv) { return (int)__builtin_amdgcn_fmed3f(__builtin_floorf(v * inv), 0.0f, top); };
@@ -660,9 +664,9 @@ __device__ __forceinline__ GridRun grid_run(float minx, float miny, float maxx, 
 }
 
 // min over the span's boxes of the separation metric (< 0: a box overlaps the segment box).
+template <class SP>
 __device__ __forceinline__ float grid_run_sep(GridRun q, float minx, float miny, float maxx, float maxy,
-                                              const KgmtDev& d) {
-    const SBMP_GAS int* const start = G(d.gridStart);
+                                              const KgmtDev& d, SP start) {
     const SBMP_GAS float4* const boxes = G(d.gridBoxes);
     const int g = d.gridG;
     const sbmp_f32x2 mn = {minx, miny}, mx = {maxx, maxy};
@@ -696,8 +700,18 @@ __device__ __forceinline__ float grid_run_sep(GridRun q, float minx, float miny,
     return sep;
 }
 
-__device__ __forceinline__ bool grid_free_fast(float minx, float miny, float maxx, float maxy, const KgmtDev& d) {
-    return !(grid_run_sep(grid_run(minx, miny, maxx, maxy, d), minx, miny, maxx, maxy, d) < 0.0f);
+template <class SP>
+__device__ __forceinline__ bool grid_free_fast(float minx, float miny, float maxx, float maxy, const KgmtDev& d,
+                                               SP start) {
+    return !(grid_run_sep(grid_run(minx, miny, maxx, maxy, d, start), minx, miny, maxx, maxy, d, start) < 0.0f);
+}
+// the table the grid query reads: LDS when the caller staged it (sStart != nullptr is
+// decided at compile time by LDSG), else global memory
+template <bool LDSG>
+__device__ __forceinline__ bool grid_free_at(float minx, float miny, float maxx, float maxy, const KgmtDev& d,
+                                             const int* sStart) {
+    if constexpr (LDSG) return grid_free_fast(minx, miny, maxx, maxy, d, (const SBMP_LDS int*)sStart);
+    else return grid_free_fast(minx, miny, maxx, maxy, d, G(d.gridStart));
 }
 
 // reference statePropagator.cu:5-76 (car).  Same operation sequence as the oracle
@@ -747,9 +761,9 @@ __device__ __forceinline__ ChildCtl draw_controls(Xorwow& rs, const KgmtDev& d) 
 // midHook() runs once, before Euler step numDisc / 2, on every lane that entered (k_step
 // issues the planner-publication loads there: late enough to see them, early enough
 // that they have landed when propagation ends).
-template <int OBS, typename MidHook = NoMidHook>
+template <int OBS, typename MidHook = NoMidHook, bool LDSG = false>
 __device__ __forceinline__ bool car_euler(float4 p, const ChildCtl& ctl, const KgmtDev& d, const float4* obs,
-                                          ChildOut& out, MidHook midHook = MidHook()) {
+                                          ChildOut& out, MidHook midHook = MidHook(), const int* sStart = nullptr) {
     const float a = ctl.a, duration = ctl.dur, dt = ctl.dt, tan_steering = ctl.tanS;
     // (x, y) and (theta, v) as float pairs: each pair update is one v_pk_mul_f32 /
     // v_pk_fma_f32 doing the same IEEE operation per component (same bits).
@@ -794,7 +808,7 @@ __device__ __forceinline__ bool car_euler(float4 p, const ChildCtl& ctl, const K
         else if (OBS == kObsGrid)   // only lanes whose result counts walk their cells
             freeSeg = oob || (d.obsNaN ? grid_motion_valid_batched(minx, miny, maxx, maxy, d.gridG, d.gridInvW,
                                                                    d.gridInvH, d.gridStart, d.gridBoxes)
-                                       : grid_free_fast(minx, miny, maxx, maxy, d));
+                                       : grid_free_at<LDSG>(minx, miny, maxx, maxy, d, sStart));
         else freeSeg = motion_valid<OBS>(minx, miny, maxx, maxy, obs, d.nObs);
         xy = nxy;
         if (!oob) tv = ntv;
@@ -819,9 +833,9 @@ __device__ __forceinline__ bool car_euler(float4 p, const ChildCtl& ctl, const K
 }
 
 // Holonomic R2 point (build extension), predicated like car_euler.
-template <int OBS, typename MidHook = NoMidHook>
+template <int OBS, typename MidHook = NoMidHook, bool LDSG = false>
 __device__ __forceinline__ bool point_euler(float4 p, const ChildCtl& ctl, const KgmtDev& d, const float4* obs,
-                                            ChildOut& out, MidHook midHook = MidHook()) {
+                                            ChildOut& out, MidHook midHook = MidHook(), const int* sStart = nullptr) {
     const float vx = ctl.a, vy = ctl.steer, duration = ctl.dur, dt = ctl.dt;
     float x = p.x, y = p.y;
     WaveCull cull{~0u, true};
@@ -840,7 +854,7 @@ __device__ __forceinline__ bool point_euler(float4 p, const ChildCtl& ctl, const
         else if (OBS == kObsGrid)
             freeSeg = oob || (d.obsNaN ? grid_motion_valid_batched(minx, miny, maxx, maxy, d.gridG, d.gridInvW,
                                                                    d.gridInvH, d.gridStart, d.gridBoxes)
-                                       : grid_free_fast(minx, miny, maxx, maxy, d));
+                                       : grid_free_at<LDSG>(minx, miny, maxx, maxy, d, sStart));
         else freeSeg = motion_valid<OBS>(minx, miny, maxx, maxy, obs, d.nObs);
         x = nx;
         y = ny;

@@ -1888,6 +1888,22 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) voi
         for (int i = tid + kBlock; i < d.nObs; i += kBlock) sObs[i] = G(d.obstacles)[i];
         __syncthreads();
     }
+    // the grid index's cell-start table into LDS: every row lookup of the Euler loop is
+    // then an LDS read instead of an L2 round trip (the boxes stay in global memory)
+    int* const sGridStart = reinterpret_cast<int*>(sNew + nW);
+    if constexpr (OBS == kObsGrid) {
+        const int nStart = d.gridG * d.gridG + 1;
+        const SBMP_GAS int* const gs = G(d.gridStart);
+        for (int i = tid; i < nStart; i += 4 * kBlock) {
+            int v[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) v[u] = (i + u * kBlock < nStart) ? gs[i + u * kBlock] : 0;
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+                if (i + u * kBlock < nStart) sGridStart[i + u * kBlock] = v[u];
+        }
+        __syncthreads();
+    }
     SBMP_STAMP(2);
     const float4* obs = (kRegObs > 0) ? ro : kLdsObs ? sObs : d.obstacles;
     ChildOut out;
@@ -1911,7 +1927,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) voi
     }
     if (!fast) {
         out = ChildOut{};   // inactive lanes: defined values (the fast loop writes every lane)
-        if (act) valid = (AGENT == 0) ? car_euler<OBS>(p, ctl, d, obs, out) : point_euler<OBS>(p, ctl, d, obs, out);
+        if (act)
+            valid = (AGENT == 0)
+                        ? car_euler<OBS, NoMidHook, OBS == kObsGrid>(p, ctl, d, obs, out, NoMidHook(), sGridStart)
+                        : point_euler<OBS, NoMidHook, OBS == kObsGrid>(p, ctl, d, obs, out, NoMidHook(), sGridStart);
     }
     SBMP_STAMP(3);
 
@@ -2288,6 +2307,7 @@ static void launch_step_form(const KgmtDev& d, int t, int expand, int variant, h
     const size_t nS = SH ? d.nBlocks / d.nranks : d.nBlocks;   // scan entries: blocks, or rows
     const size_t pfx = sizeof(int) * (nS + 1) + sizeof(uint32_t) * (size_t)(d.nR2 / 32);
     const size_t shm = sizeof(float4) * (size_t)d.nObs + pfx;   // LDS obstacle forms
+    const size_t gridLds = d.gridStart ? sizeof(int) * ((size_t)d.gridG * d.gridG + 1) : 0;   // + the cell starts
     const int blocks = SH ? d.nBlocks / d.nranks : d.nBlocks;
     const dim3 grid(1 + blocks), block(kBlock);   // workgroup 0 plans, 1.. expand
     long long* const tlBase = (d.timeline && t == d.timelineIter && expand) ? d.timeline : nullptr;
@@ -2298,7 +2318,7 @@ static void launch_step_form(const KgmtDev& d, int t, int expand, int variant, h
         cnt4, d.ctrl + (t - 1), d.rngA, d.rngB, d.gnewOut, d.status, tlBase, SH ? d.nBlocks / d.nranks : d.nBlocks, \
         SH ? reinterpret_cast<const int*>(d.stepXr + d.xCntOff) : nullptr
     if (d.gridStart) {
-        launch(k_step<AGENT, kObsGrid, SH>, grid, block, pfx, s, tm, SBMP_STEP_ARGS);
+        launch(k_step<AGENT, kObsGrid, SH>, grid, block, pfx + gridLds, s, tm, SBMP_STEP_ARGS);
     } else if (d.nObs > kMaxLdsObs) {
         launch(k_step<AGENT, kObsGlobal, SH>, grid, block, pfx, s, tm, SBMP_STEP_ARGS);
     } else if (d.nObs <= kMaxRegObs && (variant == 0 || variant == 3)) {
@@ -2330,7 +2350,10 @@ static StepFn step_fn(const KgmtDev& d, int variant, size_t* shm) {
     const size_t nS = SH ? d.nBlocks / d.nranks : d.nBlocks;
     const size_t pfx = sizeof(int) * (nS + 1) + sizeof(uint32_t) * (size_t)(d.nR2 / 32);
     *shm = pfx;
-    if (d.gridStart) return k_step<AGENT, kObsGrid, SH>;
+    if (d.gridStart) {
+        *shm = pfx + sizeof(int) * ((size_t)d.gridG * d.gridG + 1);   // + the cell-start table (k_step stages it)
+        return k_step<AGENT, kObsGrid, SH>;
+    }
     if (d.nObs > kMaxLdsObs) return k_step<AGENT, kObsGlobal, SH>;
     if (d.nObs <= kMaxRegObs && (variant == 0 || variant == 3)) {
         switch (d.nObs) {
