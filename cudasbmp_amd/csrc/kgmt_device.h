@@ -71,6 +71,7 @@ constexpr int kObsGlobal = 0;        // read from global memory, reference early
 constexpr int kObsLds = 1;           // staged in LDS, rolled loop
 constexpr int kObsLds4 = 2;          // staged in LDS, 4-way batched reads
 constexpr int kObsGrid = 3;          // uniform-grid index (include/sbmp/obstacle_grid.h), large obstacle lists
+constexpr int kMaxLdsGridG = 90;     // k_step stages the grid's (G^2 + 1)-int cell-start table in LDS: G <= 90 (32 KB)
 constexpr int kObsReg = 16;          // kObsReg + n: exactly n <= kMaxRegObs boxes held in registers
 constexpr int kMaxRegObs = 8;
 constexpr int kMaxRanks = 8;         // ranks of one sharded planning problem (one node)

@@ -603,7 +603,10 @@ void KgmtPlanner::build_grid(const float* d_obstacles, int nObs) {
     {
         std::vector<float> h((size_t)4 * nObs);
         SBMP_HIP(hipMemcpy(h.data(), d_obstacles, sizeof(float) * h.size(), hipMemcpyDeviceToHost));
-        const HostObstacleGrid g = build_obstacle_grid(h.data(), nObs, d.width, d.height, 0);
+        // k_step stages the cell-start table in LDS (G^2 + 1 ints): at most kMaxLdsGridG
+        // cells a side (32 KB); any G gives the same answers, a coarser one more boxes per cell
+        const HostObstacleGrid g =
+            build_obstacle_grid(h.data(), nObs, d.width, d.height, std::min(grid_resolution(nObs), kMaxLdsGridG));
         // kGridBatch zeroed rows past the end: grid_free_fast loads whole batches
         const size_t nStart = g.start.size(), nBoxes = g.boxes.size() + kGridBatch;
         if (nStart > gridStartCap_) {
