@@ -84,6 +84,9 @@ final)
     timeout -k 10 900 python3 -u -m pytest tests -x -q -m gpu --timeout 180 --timeout-method thread \
         -p no:cacheprovider > "$R/$out/gpu_tests.log" 2>&1 || { tail -20 "$R/$out/gpu_tests.log"; exit 1; }
     tail -1 "$R/$out/gpu_tests.log"
+    timeout -k 10 180 python3 -c "import __graft_entry__ as g; g.smoke()" > "$R/$out/smoke.log" 2>&1 \
+        || { tail -5 "$R/$out/smoke.log"; exit 1; }
+    tail -1 "$R/$out/smoke.log"
     timeout -k 10 300 python3 bench.py > "$R/$out/bench.json" 2> "$R/$out/bench.err" || { tail -5 "$R/$out/bench.err"; exit 1; }
     line "$R/$out/bench.json" default
     for rep in 1 2; do
