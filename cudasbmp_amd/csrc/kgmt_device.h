@@ -816,15 +816,15 @@ __device__ __forceinline__ bool car_euler(float4 p, const ChildCtl& ctl, const K
         alive = !oob & freeSeg;
     };
     // two loops around the hook: no per-step test of the step index
-    const int midStep = d.numDisc >> 1;
+    const int nSteps = __builtin_amdgcn_readfirstlane(d.numDisc), midStep = nSteps >> 1;
     if (d.invAgentLength != 0.0f) {
         for (int i = 0; i < midStep; ++i) step(std::true_type());
         midHook();
-        for (int i = midStep; i < d.numDisc; ++i) step(std::true_type());
+        for (int i = midStep; i < nSteps; ++i) step(std::true_type());
     } else {
         for (int i = 0; i < midStep; ++i) step(std::false_type());
         midHook();
-        for (int i = midStep; i < d.numDisc; ++i) step(std::false_type());
+        for (int i = midStep; i < nSteps; ++i) step(std::false_type());
     }
     out.state = make_float4(xy.x, xy.y, tv.x, tv.y);
     out.a = a;
@@ -861,10 +861,10 @@ __device__ __forceinline__ bool point_euler(float4 p, const ChildCtl& ctl, const
         y = ny;
         alive = !oob & freeSeg;
     };
-    const int midStep = d.numDisc >> 1;
+    const int nSteps = __builtin_amdgcn_readfirstlane(d.numDisc), midStep = nSteps >> 1;
     for (int i = 0; i < midStep; ++i) step();
     midHook();
-    for (int i = midStep; i < d.numDisc; ++i) step();
+    for (int i = midStep; i < nSteps; ++i) step();
     out.state = make_float4(x, y, 0.0f, 0.0f);
     out.a = vx;
     out.steer = vy;
@@ -1004,7 +1004,10 @@ __device__ __forceinline__ bool car_euler_fast(float4 p, const ChildCtl& ctl, co
     const unsigned kept = __builtin_amdgcn_readfirstlane(cull.boxes);   // wave-uniform (a ballot)
     unsigned long long sb = sched.boxes, sw = cull.bounds ? sched.bounds : 0ull;   // uniform
     float aliveF = 1.0f;   // 1 alive, 0 ended: a float, so no lane mask is carried across steps
-    for (int i = 0; i < d.numDisc; ++i) {
+    // the step count in a register: read through d in the loop condition, it was re-loaded
+    // (s_load + lgkmcnt wait) every step, the inline asm below being opaque to alias analysis
+    const int nSteps = __builtin_amdgcn_readfirstlane(d.numDisc);
+    for (int i = 0; i < nSteps; ++i) {
         // re-tested every step (s_bitcmp1 + branch): hoisted, each kept flag would hold
         // a 64-bit lane mask in scalar registers for the whole loop
         unsigned keptNow = kept & (unsigned)sb;
