@@ -13,6 +13,7 @@
 #   tools/gpu_cycle.sh trace <out> [bench args]    rocprofv3 --kernel-trace --stats of a bench run
 #   tools/gpu_cycle.sh bench <out> <name> [args]   one bench line into <out>/<name>.json
 #   tools/gpu_cycle.sh shard <out>                 tools/shard_cost.py 1 2 8 and two ranks on one GPU
+#   tools/gpu_cycle.sh attrib <out> <wl> <n> <it>  per-launch traffic fitted per child (tools/write_attrib.py)
 #   tools/gpu_cycle.sh microbench <out>            build and run tools/microbench/{valu,salu}_bench
 #   tools/gpu_cycle.sh final <out>                 the round's record: pytest -m gpu, the default bench line,
 #                                                  two driver-form lines, a 300-step line, the rocprofv3
@@ -104,6 +105,16 @@ final)
     timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$R/$out/trace" -o run --output-format csv -- \
         python3 "$R/bench.py" --no-cpu-baseline > "$R/$out/bench_traced.json" 2> "$R/$out/bench_traced.err" || exit 1
     cd "$R" && line "$out/bench_traced.json" traced ;;
+attrib)   # <workload> <samples> <iterations>: per-launch WRITE_SIZE / FETCH_SIZE fitted per unit of work
+    wl=$1; ns=$2; it=$3; mkdir -p "$R/$out/$wl"; cd /tmp && export TMPDIR=/tmp
+    for c in WRITE_SIZE FETCH_SIZE; do
+        d=$(echo "$c" | cut -d_ -f1 | tr A-Z a-z)
+        timeout -s KILL 120 rocprofv3 --pmc "$c" -d "$R/$out/$wl/$d" -o run --output-format csv -- \
+            python3 "$R/tools/write_attrib.py" run "$wl" "$ns" "$it" "$R/$out/$wl/log.json" \
+            > "$R/$out/$wl/$d.log" 2>&1 || { tail -5 "$R/$out/$wl/$d.log"; exit 1; }
+    done
+    cd "$R" && python3 tools/write_attrib.py fit "$out/$wl/log.json" "$out/$wl/write" "$out/$wl/fetch" \
+        > "$out/$wl/fit.txt" && head -8 "$out/$wl/fit.txt" ;;
 microbench)
     for b in valu_bench salu_bench; do
         /opt/rocm/bin/hipcc -O3 --offload-arch=gfx950 "tools/microbench/$b.hip" -o "/tmp/$b" || exit 1
