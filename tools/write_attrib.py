@@ -76,6 +76,18 @@ def fit(logpath, write_dir, fetch_dir, skip=3):
     tot = (wr[:n] + rd[:n])[sl]
     print(f"  mean S {S[:n][sl].mean():.0f}  mean traffic {tot.mean() / 1e6:.3f} MB  mean algorithmic "
           f"{alg.mean() / 1e6:.3f} MB  ratio {tot.mean() / alg.mean():.3f}")
+    idle = [i for i in range(skip, n) if S[i] == 0]
+    busy = [i for i in range(skip, n) if S[i] > 0]
+    if busy:
+        a_b = 81.0 * S[busy] + 20.0 * nG[busy]
+        print(f"  {len(busy)} launches with S > 0: write {wr[busy].mean() / 1e6:.3f} MB, read {rd[busy].mean() / 1e6:.3f} MB "
+              f"against algorithmic {a_b.mean() / 1e6:.3f} MB (writes 57 B/child: {57.0 * S[busy].mean() / 1e6:.3f}, "
+              f"reads 24 B/child + 20 B/frontier: {(24.0 * S[busy] + 20.0 * nG[busy]).mean() / 1e6:.3f}); ratio "
+              f"{(wr[busy] + rd[busy]).mean() / a_b.mean():.3f}")
+    if idle:   # launches that expand nothing: what every launch reads whatever its S
+        print(f"  {len(idle)} launches with S = 0: write {wr[idle].mean() / 1e3:.1f} KB, read {rd[idle].mean() / 1e3:.1f} KB; "
+              f"the RNG state of every slot (24 B x {L['samples']}, loaded at entry before the plan) = "
+              f"{24.0 * L['samples'] / 1e3:.1f} KB")
     print("   t        S      A(t-1)   nG    write KB   read KB   algorithmic KB")
     for i in range(skip, n):
         print(f"  {int(log[i, 0]):3d} {int(S[i]):8d} {int(Aprev[i]):8d} {int(nG[i]):6d} {wr[i] / 1e3:10.1f} "
