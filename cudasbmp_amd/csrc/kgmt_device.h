@@ -283,6 +283,16 @@ __device__ __forceinline__ void store_wt(uint4* base, int i, uint4 v) {
 __device__ __forceinline__ void store_wt(uint2* base, int i, uint2 v) {
     __builtin_amdgcn_raw_buffer_store_b64(sbmp_u32x2{v.x, v.y}, wt_rsrc(base), SBMP_WT_OFF(i, 8), kCpolSc1);
 }
+__device__ __forceinline__ void store_wt(unsigned long long* base, int i, unsigned long long v) {
+    __builtin_amdgcn_raw_buffer_store_b64(sbmp_u32x2{(uint32_t)v, (uint32_t)(v >> 32)}, wt_rsrc(base), SBMP_WT_OFF(i, 8),
+                                          kCpolSc1);
+}
+__device__ __forceinline__ void store_wt(int* base, int i, int v) {
+    __builtin_amdgcn_raw_buffer_store_b32((uint32_t)v, wt_rsrc(base), SBMP_WT_OFF(i, 4), kCpolSc1);
+}
+__device__ __forceinline__ void store_wt(uint16_t* base, int i, uint16_t v) {
+    __builtin_amdgcn_raw_buffer_store_b16(v, wt_rsrc(base), SBMP_WT_OFF(i, 2), kCpolSc1);
+}
 
 // Slot i's XORWOW state for i < n, zeros with no memory access for i >= n: the
 // buffer's num_records is the n slots' bytes, and a raw buffer load whose offset is

@@ -1770,9 +1770,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) voi
                 const float4 s4 = list_load<SH>(d, e);
                 const float4 u4 = list_load<SH>(d, e + 1);
                 const float4 m4 = list_load<SH>(d, e + 2);
-                G(d.treeState)[dst] = s4;
-                G(d.treeCtrl)[dst] = make_float4(u4.x, u4.y, u4.z, m4.x);   // cost = parent's + duration (KGMT.cu:631-633)
-                G(d.treeParent)[dst] = __float_as_int(u4.w);
+                // written through (fewer dirty lines at the boundary); the V# based at row tsPrev keeps
+                // the byte offset j * 16 far below 2^31 whatever M is
+                store_wt(d.treeState + q.tsPrev, j, s4);
+                store_wt(d.treeCtrl + q.tsPrev, j, make_float4(u4.x, u4.y, u4.z, m4.x));   // cost = parent's + duration (KGMT.cu:631-633)
+                store_wt(d.treeParent + q.tsPrev, j, __float_as_int(u4.w));
             }
         }
     };
@@ -1791,9 +1793,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) voi
                         const float4 s4 = list_load<SH>(d, e);
                         const float4 u4 = list_load<SH>(d, e + 1);
                         const float4 m4 = list_load<SH>(d, e + 2);
-                        G(d.treeState)[dst] = s4;
-                        G(d.treeCtrl)[dst] = make_float4(u4.x, u4.y, u4.z, m4.x);
-                        G(d.treeParent)[dst] = __float_as_int(u4.w);
+                        store_wt(d.treeState + q.tsPrev, j, s4);
+                        store_wt(d.treeCtrl + q.tsPrev, j, make_float4(u4.x, u4.y, u4.z, m4.x));
+                        store_wt(d.treeParent + q.tsPrev, j, __float_as_int(u4.w));
                     }
                 }
             } else {
@@ -1967,8 +1969,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) voi
         store_wt(d.rngB, slot, make_uint2(rs.v4, rs.d));
         if (q1 >= 0) atomicAdd(&sR1P[q1], valid ? 1 : 0x10000);
         if (d.r2log) {
-            G(d.r2log)[(size_t)(t % kFoldEvery) * d.logSlots + b * kBlock + tid] =
-                (q2 >= 0) ? (uint16_t)(q2 | (valid ? 0x8000 : 0)) : kNoKey;
+            store_wt(d.r2log, (t % kFoldEvery) * d.logSlots + b * kBlock + tid,
+                     (q2 >= 0) ? (uint16_t)(q2 | (valid ? 0x8000 : 0)) : kNoKey);
         } else if (q2 >= 0) {
             __hip_atomic_fetch_add(G(valid ? d.R2Valid : d.R2Invalid) + q2, 1, __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_AGENT);
@@ -2026,7 +2028,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) voi
     const int idxW = __builtin_amdgcn_mbcnt_hi((uint32_t)(wordAll >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)wordAll, 0u));
     const int glW = first_lane_value(flagged && inGoal, idxW, kNoGoalIdx);
     if (lane == 0) {
-        G(d.gnewOut)[slot >> 6] = wordAll;
+        store_wt(d.gnewOut, slot >> 6, wordAll);
         sWaveCnt[wave] = __popcll(wordAll);
         sWaveGoal[wave] = glW;
     }
@@ -2063,11 +2065,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) voi
             __builtin_amdgcn_raw_buffer_store_b128(sbmp_u32x4{__float_as_uint(cc.x), __float_as_uint(cc.y), __float_as_uint(cc.z), __float_as_uint(cc.w)}, rl, vo + 16, so, 0);
             __builtin_amdgcn_raw_buffer_store_b128(sbmp_u32x4{__float_as_uint(cost), 0u, 0u, 0u}, rl, vo + 32, so, 0);
 #else
-            SBMP_GAS float4* e =
-                G(d.stepList) + ((size_t)cp * d.nBlocks * kBlock + (size_t)b * kBlock + waveOff + idxW) * kStepEntry;
-            e[0] = cs;
-            e[1] = cc;
-            e[2] = make_float4(cost, 0.0f, 0.0f, 0.0f);
+            const int e = (cp * d.nBlocks * kBlock + b * kBlock + waveOff + idxW) * kStepEntry;   // < 2^27 entries
+            store_wt(d.stepList, e, cs);
+            store_wt(d.stepList, e + 1, cc);
+            store_wt(d.stepList, e + 2, make_float4(cost, 0.0f, 0.0f, 0.0f));
 #endif
         }
     }
