@@ -1518,10 +1518,10 @@ __device__ __forceinline__ void step_planner(const KgmtDev& d, const ShardView& 
         for (int i = tid; i < kDeltaReps * d.nR1; i += kBlock) zx[i] = 0ull;
         for (int i = tid; i < d.nR2 / 8; i += kBlock) zx[d.xNewOff + i] = 0ull;   // R2New bytes (count words: owner-written)
     } else {   // ring (t+1) % 3, last read by k_step(t-1): zero for k_step(t+1)
-        SBMP_GAS unsigned long long* zd = G(d.stepDelta) + (size_t)((t + 1) % 3) * kDeltaReps * d.nR1;
-        for (int i = tid; i < kDeltaReps * d.nR1; i += kBlock) zd[i] = 0ull;
-        SBMP_GAS uint32_t* zn = G(d.stepR2New) + (size_t)((t + 1) % 3) * kNewReps * nW;
-        for (int i = tid; i < kNewReps * nW; i += kBlock) zn[i] = 0u;
+        unsigned long long* const zd = d.stepDelta + (size_t)((t + 1) % 3) * kDeltaReps * d.nR1;   // written through
+        for (int i = tid; i < kDeltaReps * d.nR1; i += kBlock) store_wt(zd, i, 0ull);
+        int* const zn = reinterpret_cast<int*>(d.stepR2New + (size_t)((t + 1) % 3) * kNewReps * nW);
+        for (int i = tid; i < kNewReps * nW; i += kBlock) store_wt(zn, i, 0);
     }
     if (tid == 0) {
         IterCtrl c;
@@ -1561,11 +1561,10 @@ __device__ __forceinline__ void step_planner(const KgmtDev& d, const ShardView& 
                 return list_entry<SH>(d, pp, lo, j - sPfx[lo]);
             }
         };
-        auto put = [&](int j, float4 s4, float4 u4, float c) {
-            const int dst = q.tsPrev + j;
-            G(d.treeState)[dst] = s4;
-            G(d.treeCtrl)[dst] = make_float4(u4.x, u4.y, u4.z, c);   // cost = parent's + duration (KGMT.cu:631-633)
-            G(d.treeParent)[dst] = __float_as_int(u4.w);
+        auto put = [&](int j, float4 s4, float4 u4, float c) {   // row tsPrev + j, written through
+            store_wt(d.treeState + q.tsPrev, j, s4);
+            store_wt(d.treeCtrl + q.tsPrev, j, make_float4(u4.x, u4.y, u4.z, c));   // cost = parent's + duration (KGMT.cu:631-633)
+            store_wt(d.treeParent + q.tsPrev, j, __float_as_int(u4.w));
         };
         for (int j0 = tid; j0 < n; j0 += 2 * kBlock) {   // two rows per thread per round, loads first
             const int j1 = j0 + kBlock;
