@@ -78,7 +78,11 @@ constexpr int kMaxRanks = 8;         // ranks of one sharded planning problem (o
 constexpr int obs_in_registers(int obs) { return obs >= kObsReg ? obs - kObsReg : 0; }
 constexpr int kTimelineStamps = 8;   // s_memrealtime stamps per k_expand wave (diagnostics)
 constexpr int kFoldEvery = 32;       // iterations per R2 key-log fold (k_fold_r2; 32: 0.51 us per iteration vs 0.87 at 16)
-constexpr int kFoldKeys = 65280;     // keys per fold workgroup (< 2^16: packed 16-bit LDS counters)
+#ifndef SBMP_FOLD_KEYS
+#define SBMP_FOLD_KEYS 65280
+#endif
+constexpr int kFoldKeys = SBMP_FOLD_KEYS;   // keys per fold workgroup (< 2^16: packed 16-bit LDS counters; a multiple of 8)
+static_assert(kFoldKeys % 8 == 0 && kFoldKeys < 65536, "fold: whole 8-key loads, 16-bit counters");
 constexpr int kLogMaxR2 = 32767;     // the 16-bit key (r2 | valid << 15) holds r2 < 32767
 constexpr uint16_t kNoKey = 0xffff;  // child outside the R2 grid (D3)
 // R1 delta replicas [kDeltaReps][nR1]: workgroup b adds to replica b % kDeltaReps.
