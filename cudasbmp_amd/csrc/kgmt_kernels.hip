@@ -1000,7 +1000,9 @@ __device__ __forceinline__ void k_step_exchange(const KgmtDev& d, int nranks, in
         if ((int)old + 1 == expect) {   // the shard's last arrival: worker `shard`, once every shard is in
             __hip_atomic_fetch_add(arr + 8 * kFxStride, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
-            while ((int)__hip_atomic_load(arr + 8 * kFxStride, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < nW) {
+            // + 1: the planner workgroup's own arrival (step_planner_arrive), after its last read of
+            // recv, which the workers overwrite
+            while ((int)__hip_atomic_load(arr + 8 * kFxStride, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < nW + 1) {
                 if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > kExchangeWaitTicks) {   // report, do not hang
                     atomicExch(&d.status->error, kErrExchange);
                     break;
@@ -1083,7 +1085,83 @@ __device__ __forceinline__ void k_step_exchange(const KgmtDev& d, int nranks, in
     if (fxTl) fxTl[5] = (long long)__builtin_amdgcn_s_memrealtime();
 }
 
+// The planner workgroup of a fused-exchange k_step(t) reads t-1's recv (row, block and
+// delta words, R2New bytes) at entry and, while it inserts t-1's rows, the block words of
+// their rows; the workers of exchange t rewrite recv.  So it arrives too, once its loads
+// have returned (every wave's vmcnt(0), then a barrier): one add to the top counter,
+// which the workers wait for besides the shards' (ADVICE r04).
+__device__ __forceinline__ void step_planner_arrive(const KgmtDev& d, int t) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0)
+        __hip_atomic_fetch_add(G(d.xArrive) + ((size_t)(t & 1) * kFxCounters + 8) * kFxStride, 1u, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+}
+
 size_t oneshot_inbox_words(long long n, int nranks) { return (size_t)2 * nranks * n + (size_t)nranks * kOneshotChunks; }
+
+// ------------------------------------------------------------------ list-mirror check
+// The start-up check of the list mirror (KgmtPlanner::mirror_self_test):
+// every rank's k_step stores its flagged children's entries into every peer's mirror with
+// system-scope stores, and each rank reads its own mirror in its next k_step with plain
+// loads, relying on the kernel boundary in between to drop lines its L2 still holds from
+// two iterations back.  The check reproduces exactly that: touch (plain loads of the probed
+// entries, so they sit in this GPU's caches), a host barrier, push (every rank stores a
+// pass-specific pattern into the entries of its own global blocks in every rank's mirror,
+// as k_step does), a host barrier, check (a new launch reads them with plain loads and
+// compares).  Two passes, so that pass 1 finds pass 0's lines cached.
+__device__ __forceinline__ float4 probe_entry(int writer, int g, int i, int k, int pass) {
+    const uint32_t h = (uint32_t)(writer * 0x9E3779B1u) ^ (uint32_t)(g * 0x85EBCA77u) ^ (uint32_t)(i * 0xC2B2AE3Du) ^
+                       (uint32_t)(k * 0x27D4EB2Fu) ^ (uint32_t)((pass + 1) * 0x165667B1u);
+    return make_float4(__uint_as_float(h & 0x7f7fffffu), __uint_as_float((h * 3u) & 0x7f7fffffu),
+                       __uint_as_float((h ^ 0x5bd1e995u) & 0x7f7fffffu), __uint_as_float((h + 0x68e31da4u) & 0x7f7fffffu));
+}
+// entry (parity, global block g, index i) of the probed set: parity-major, one thread each
+__device__ __forceinline__ size_t probe_index(const MirrorProbe& a, int e, int* g, int* i) {
+    const int par = e / (a.blocks * a.entries), r = e % (a.blocks * a.entries);
+    *g = r / a.entries;
+    *i = r % a.entries;
+    return ((size_t)par * a.nBlocks + *g) * kBlock * kStepEntry + (size_t)*i * kStepEntry;
+}
+__global__ void k_mirror_touch(MirrorProbe a, float* sink) {
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= 2 * a.blocks * a.entries) return;
+    int g, i;
+    const size_t o = probe_index(a, e, &g, &i);
+    float acc = 0.0f;
+    for (int k = 0; k < kStepEntry; ++k) acc += G(a.own)[o + k].x;   // plain loads, as k_step's
+    if (acc == 1.2345f) sink[0] = acc;   // keeps the loads
+}
+__global__ void k_mirror_push(MirrorProbe a, int pass) {
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= 2 * a.blocks * a.entries) return;
+    int g, i;
+    const size_t o = probe_index(a, e, &g, &i);
+    if (g % a.nranks != a.rank) return;   // this rank's global blocks only, as k_step
+    for (int q = 0; q < a.nranks; ++q)
+        for (int k = 0; k < kStepEntry; ++k) store_record_g(G(a.peer[q]) + o + k, probe_entry(a.rank, g, i, k, pass));
+}
+__global__ void k_mirror_check(MirrorProbe a, int pass) {
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= 2 * a.blocks * a.entries) return;
+    int g, i;
+    const size_t o = probe_index(a, e, &g, &i);
+    int bad = 0;
+    for (int k = 0; k < kStepEntry; ++k) {
+        const float4 v = G(a.own)[o + k];   // plain loads, as k_step's
+        const float4 w = probe_entry(g % a.nranks, g, i, k, pass);
+        bad += (__float_as_uint(v.x) != __float_as_uint(w.x)) | (__float_as_uint(v.y) != __float_as_uint(w.y)) |
+               (__float_as_uint(v.z) != __float_as_uint(w.z)) | (__float_as_uint(v.w) != __float_as_uint(w.w));
+    }
+    if (bad) atomicAdd(a.bad, bad);
+}
+void launch_mirror_probe(const MirrorProbe& a, int phase, int pass, float* sink, hipStream_t s) {
+    const int n = 2 * a.blocks * a.entries;
+    const dim3 grid((n + kBlock - 1) / kBlock), block(kBlock);
+    if (phase == 0) hipLaunchKernelGGL(k_mirror_touch, grid, block, 0, s, a, sink);
+    else if (phase == 1) hipLaunchKernelGGL(k_mirror_push, grid, block, 0, s, a, pass);
+    else hipLaunchKernelGGL(k_mirror_check, grid, block, 0, s, a, pass);
+}
 
 
 // ------------------------------------------------------------------ step
@@ -1105,11 +1183,89 @@ size_t oneshot_inbox_words(long long n, int nranks) { return (size_t)2 * nranks 
 // expand == 0 is the flush pass run before a read-back (no expansion; the same
 // values are rewritten by k_step(t) proper, so it is idempotent).
 // OR of word w over the kNewReps R2New replicas ([rep][nW] layout: one line per replica)
-__device__ __forceinline__ uint32_t merge_new(const SBMP_GAS uint32_t* p, int nW, int w) {
+// of ring slot `ring` (sc1 loads: the overlapped form reads them behind step_wait_prev)
+__device__ __forceinline__ uint32_t merge_new(const KgmtDev& d, int ring, int nW, int w) {
     uint32_t v = 0u;
 #pragma unroll
-    for (int r = 0; r < kNewReps; ++r) v |= p[(size_t)r * nW + w];
+    for (int r = 0; r < kNewReps; ++r) v |= ld_sc1_x1(d.stepR2New, (int)(((size_t)(ring * kNewReps + r) * nW + w) * 4));
     return v;
+}
+
+// ctrl[t-1] with sc1 loads (fields run .. scoreBuf: three 16-B loads of the 64-B line)
+__device__ __forceinline__ IterCtrl ld_ctrl(const IterCtrl* p) {
+    const sbmp_u32x4 a = ld_sc1_x4(p, 0), b = ld_sc1_x4(p, 16), c = ld_sc1_x4(p, 32);
+    IterCtrl r;
+    r.run = (int)a[0];
+    r.executed = (int)a[1];
+    r.treeSize = (int)a[2];
+    r.gLo = (int)a[3];
+    r.nG = (int)b[0];
+    r.k = (int)b[1];
+    r.nExp = (int)b[2];
+    r.S = (int)b[3];
+    r.H = (int)c[0];
+    r.A = (int)c[1];
+    r.scoreBuf = (int)c[2];
+    for (int i = 0; i < 5; ++i) r.pad[i] = 0;
+    return r;
+}
+// ctrl[t] written through (lane-uniform value, one thread stores)
+__device__ __forceinline__ void st_ctrl(IterCtrl* base, int t, const IterCtrl& c) {
+    uint4* const q = reinterpret_cast<uint4*>(base + t);
+    store_wt(q, 0, make_uint4(c.run, c.executed, c.treeSize, c.gLo));
+    store_wt(q, 1, make_uint4(c.nG, c.k, c.nExp, c.S));
+    store_wt(q, 2, make_uint4(c.H, c.A, c.scoreBuf, c.pad[0]));
+    store_wt(q, 3, make_uint4(c.pad[1], c.pad[2], c.pad[3], c.pad[4]));
+}
+
+// ---- overlapped k_step: consecutive launches on two alternating
+// streams, with no stream dependency between them; launch t's workgroups wait here for
+// every workgroup of launch t-1 instead of a kernel boundary.  The hand-off is the
+// guide's "sc1 stores, drained, one agent-scope add per workgroup, sc1 loads" row
+// (MI355X_MICROARCH.md, inter-workgroup visibility): everything k_step writes for a
+// later launch is stored sc1 (store_wt, atomics), every wave drains its stores before
+// its workgroup arrives, and every load of those bytes is an sc1 load.
+// The counters (kDoneWordOff, kgmt_device.h) sit behind the status block.
+__device__ __forceinline__ SBMP_GAS unsigned* done_counters(const PlannerStatus* st) {
+    return (SBMP_GAS unsigned*)(const_cast<PlannerStatus*>(st)) + kDoneWordOff;   // C cast: address space
+}
+// One lane polls the top counter (relaxed sc1 loads, s_sleep between) until the shards
+// of launch t-1 are all in (shards per launch: min(8, workgroups)); the other waves wait
+// at the barrier.  Bounded: a timeout sets status.error, which the host raises.
+__device__ __forceinline__ void step_wait_prev(const PlannerStatus* st, int t, int shards) {
+    if (threadIdx.x == 0 && t > 1) {
+        const SBMP_GAS unsigned* const top = done_counters(st) + 8 * kFxStride;
+        const unsigned want = (unsigned)(t - 1) * (unsigned)shards;
+        if ((int)(__hip_atomic_load(top, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - want) < 0) {
+            const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
+            for (;;) {
+                __builtin_amdgcn_s_sleep(2);
+                if ((int)(__hip_atomic_load(top, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - want) >= 0) break;
+                if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > kStepWaitTicks) {   // report, do not hang
+                    __hip_atomic_exchange(&G(const_cast<PlannerStatus*>(st))->error, kErrStepOverlap, __ATOMIC_RELAXED,
+                                          __HIP_MEMORY_SCOPE_AGENT);
+                    break;
+                }
+            }
+        }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // no instruction: keeps the loads below the poll
+    __syncthreads();
+}
+// Every wave's stores have completed, then lane 0 adds one to its shard (workgroup index
+// mod 8); the shard's last arrival of launch t (its count reaches t x its workgroups per
+// launch: arrivals of t+1 cannot start before all of t's) adds one to the top counter.
+__device__ __forceinline__ void step_arrive(const PlannerStatus* st, int t, int groups) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        SBMP_GAS unsigned* const c = done_counters(st);
+        const int s = (int)(blockIdx.x & 7);
+        const unsigned per = (unsigned)((groups - s + 7) >> 3);
+        const unsigned old = __hip_atomic_fetch_add(c + s * kFxStride, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (old + 1u == (unsigned)t * per)
+            __hip_atomic_fetch_add(c + 8 * kFxStride, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
 }
 
 __device__ __forceinline__ void step_unpack(int v, int* cnt, int* goal) {
@@ -1286,6 +1442,11 @@ __device__ __forceinline__ float4 list_load(const KgmtDev& d, const SBMP_GAS flo
     if (SH && !d.listPlain) return load_record_g(p);
     return *p;
 }
+// A single rank's list entry of row j: byte offset of (block lo, index i) in stepList
+// ([2][nBlocks * kBlock][kStepEntry] float4: < 2^31 B), read with sc1 loads.
+__device__ __forceinline__ int list_off(const KgmtDev& d, int pp, int lo, int i) {
+    return (int)((((size_t)pp * d.nBlocks + lo) * kBlock + i) * kStepEntry * 16);
+}
 
 // Plan scalars of iteration t from t-1's control block and the scan (KGMT.cu:118,
 // 139-188,249-259); every workgroup derives the same values.
@@ -1358,26 +1519,31 @@ __device__ __forceinline__ void step_planner(const KgmtDev& d, const ShardView& 
     if (tl) G(d.timelineFin)[0] = (long long)__builtin_amdgcn_s_memrealtime();
     // every input at entry
     // t-1's packed counts: blocks, or (sharded) rows of the exchange
-    const int4 pk = SH ? reinterpret_cast<const SBMP_GAS int4*>(G(d.stepXr) + d.xRowOff)[tid]
-                       : *reinterpret_cast<const SBMP_GAS int4*>(G(d.stepCnt) + (size_t)pp * kMaxStepBlocks + tid * 4);
-    const IterCtrl pc = G(d.ctrl)[t - 1];
-    const int goalIdx = G(d.status)->goalIdx;
-    const SBMP_GAS int* tabPrev = G(d.R1) + (size_t)pp * 5 * d.nR1;
-    int r1 = tabPrev[cell], r1a = tabPrev[d.nR1 + cell], r1v = tabPrev[2 * d.nR1 + cell],
-        r1i = tabPrev[3 * d.nR1 + cell], r1c = tabPrev[4 * d.nR1 + cell];
+    // Everything k_step(t-1) (or earlier) wrote is read with sc1 loads (the overlapped
+    // form, step_wait_prev); the plan struct and the obstacles are constant.
+    const int4 pk = SH ? ld_sc1_i4(d.stepXr + d.xRowOff, tid * 16) : ld_sc1_i4(d.stepCnt, (pp * kMaxStepBlocks + tid * 4) * 4);
+    const IterCtrl pc = ld_ctrl(d.ctrl + (t - 1));
+    const int goalIdx = (int)ld_sc1_x1(d.status, 0);
+    const int* const tabPrev = d.R1 + (size_t)pp * 5 * d.nR1;
+    int r1 = (int)ld_sc1_x1(tabPrev, cell * 4), r1a = (int)ld_sc1_x1(tabPrev, (d.nR1 + cell) * 4),
+        r1v = (int)ld_sc1_x1(tabPrev, (2 * d.nR1 + cell) * 4), r1i = (int)ld_sc1_x1(tabPrev, (3 * d.nR1 + cell) * 4),
+        r1c = (int)ld_sc1_x1(tabPrev, (4 * d.nR1 + cell) * 4);
     // sharded: the exchange's sum over ranks; else ring (t - 1) % 3
-    const SBMP_GAS unsigned long long* deltaPrev =
-        SH ? G(d.stepXr) : G(d.stepDelta) + (size_t)((t - 1) % 3) * kDeltaReps * d.nR1;
     unsigned long long dl = 0ull;   // replicas: carry-free sums
+    if constexpr (SH) {
 #pragma unroll
-    for (int r = 0; r < kDeltaReps; ++r) dl += deltaPrev[(size_t)r * d.nR1 + cell];
-    const SBMP_GAS uint32_t* availPrev = G(d.R2Avail) + (size_t)pp * nW;
-    const SBMP_GAS uint32_t* newPrev = G(d.stepR2New) + (size_t)((t - 1) % 3) * kNewReps * nW;
+        for (int r = 0; r < kDeltaReps; ++r) dl += G(d.stepXr)[(size_t)r * d.nR1 + cell];
+    } else {
+        const unsigned long long* const deltaPrev = d.stepDelta + (size_t)((t - 1) % 3) * kDeltaReps * d.nR1;
+#pragma unroll
+        for (int r = 0; r < kDeltaReps; ++r) dl += ld_sc1_u64(deltaPrev, (r * d.nR1 + cell) * 8);
+    }
+    const uint32_t* const availPrev = d.R2Avail + (size_t)pp * nW;
     uint32_t availW[kW], newW[kW];
 #pragma unroll
     for (int j = 0; j < kW; ++j) {
         const int w = min(tid + j * kBlock, nW - 1);
-        availW[j] = availPrev[w];
+        availW[j] = ld_sc1_x1(availPrev, w * 4);
         newW[j] = 0u;
     }
     // the R2New replicas: n <= 8 (two words per thread) with all 16 loads in flight;
@@ -1402,12 +1568,12 @@ __device__ __forceinline__ void step_planner(const KgmtDev& d, const ShardView& 
             }
         }
     } else if (nW <= 2 * kBlock) {
-        newW[0] = merge_new(newPrev, nW, min(tid, nW - 1));
-        newW[1] = merge_new(newPrev, nW, min(tid + kBlock, nW - 1));
+        newW[0] = merge_new(d, (t - 1) % 3, nW, min(tid, nW - 1));
+        newW[1] = merge_new(d, (t - 1) % 3, nW, min(tid + kBlock, nW - 1));
     } else {
 #pragma unroll
         for (int j = 0; j < kW; ++j)
-            if (j * kBlock < nW) newW[j] = merge_new(newPrev, nW, min(tid + j * kBlock, nW - 1));
+            if (j * kBlock < nW) newW[j] = merge_new(d, (t - 1) % 3, nW, min(tid + j * kBlock, nW - 1));
     }
     for (int i = tid; i < d.nR1; i += kBlock) sCovInc[i] = 0;
     int A, jGoal;
@@ -1420,15 +1586,15 @@ __device__ __forceinline__ void step_planner(const KgmtDev& d, const ShardView& 
         step_scan(d, pk, sPfx, sRed, &A, &jGoal);
     }
     const StepPlan q = step_plan(d, t, expand, pc, goalIdx, A, jGoal);
-    SBMP_GAS int* tabCur = G(d.R1) + (size_t)cp * 5 * d.nR1;
+    int* const tabCur = d.R1 + (size_t)cp * 5 * d.nR1;   // written through, like everything below
     if (!q.ranPrev) {   // t-1 did not run: the loop has ended; carry the tables forward
-        for (int i = tid; i < 5 * d.nR1; i += kBlock) tabCur[i] = tabPrev[i];
-        for (int i = tid; i < nW; i += kBlock) G(d.R2Avail)[(size_t)cp * nW + i] = availPrev[i];
+        for (int i = tid; i < 5 * d.nR1; i += kBlock) store_wt(tabCur, i, (int)ld_sc1_x1(tabPrev, i * 4));
+        for (int i = tid; i < nW; i += kBlock) store_wt(d.R2Avail + (size_t)cp * nW, i, ld_sc1_x1(availPrev, i * 4));
         if (tid == 0) {
             IterCtrl c{};
             c.run = 0;
             c.H = pc.H;
-            G(d.ctrl)[t] = c;
+            st_ctrl(d.ctrl, t, c);
         }
         return;
     }
@@ -1498,17 +1664,17 @@ __device__ __forceinline__ void step_planner(const KgmtDev& d, const ShardView& 
     }
     if (tl) G(d.timelineFin)[1] = (long long)__builtin_amdgcn_s_memrealtime();
     if (own) {
-        tabCur[cell] = r1;
-        tabCur[d.nR1 + cell] = r1a;
-        tabCur[2 * d.nR1 + cell] = r1v;
-        tabCur[3 * d.nR1 + cell] = r1i;
-        tabCur[4 * d.nR1 + cell] = r1c;
-        if (q.runT) G(d.R1Score)[cp * d.nR1 + cell] = scv;
+        store_wt(tabCur, cell, r1);
+        store_wt(tabCur, d.nR1 + cell, r1a);
+        store_wt(tabCur, 2 * d.nR1 + cell, r1v);
+        store_wt(tabCur, 3 * d.nR1 + cell, r1i);
+        store_wt(tabCur, 4 * d.nR1 + cell, r1c);
+        if (q.runT) store_wt(d.R1Score, cp * d.nR1 + cell, scv);
     }
 #pragma unroll
     for (int j = 0; j < kW; ++j) {
         const int w = tid + j * kBlock;
-        if (j * kBlock < nW && w < nW) G(d.R2Avail)[(size_t)cp * nW + w] = snapW[j];
+        if (j * kBlock < nW && w < nW) store_wt(d.R2Avail + (size_t)cp * nW, w, snapW[j]);
     }
     if constexpr (SH) {   // send parity (t+1) & 1, last read by exchange t-1: zero for k_step(t+1)
         if (d.fusedX && tid < kFxCounters)   // and the fused exchange's arrival counters of t+1
@@ -1537,9 +1703,9 @@ __device__ __forceinline__ void step_planner(const KgmtDev& d, const ShardView& 
         c.A = 0;
         c.scoreBuf = cp;
         for (int i = 0; i < 5; ++i) c.pad[i] = 0;
-        G(d.ctrl)[t] = c;
-        if (t > 1) G(d.ctrl)[t - 1].A = A;
-        if (q.newGoal != goalIdx) G(d.status)->goalIdx = q.newGoal;
+        st_ctrl(d.ctrl, t, c);
+        if (t > 1) store_wt(reinterpret_cast<int*>(d.ctrl + (t - 1)), 9, A);   // .A
+        if (q.newGoal != goalIdx) store_wt(reinterpret_cast<int*>(d.status), 0, q.newGoal);   // .goalIdx
     }
     // Insert t-1's flagged children (rows tsPrev + j, KGMT.cu:540-593) when they are
     // few: everything above is what the expanders wait for, and from here on this
@@ -1566,15 +1732,34 @@ __device__ __forceinline__ void step_planner(const KgmtDev& d, const ShardView& 
             store_wt(d.treeCtrl + q.tsPrev, j, make_float4(u4.x, u4.y, u4.z, c));   // cost = parent's + duration (KGMT.cu:631-633)
             store_wt(d.treeParent + q.tsPrev, j, __float_as_int(u4.w));
         };
-        for (int j0 = tid; j0 < n; j0 += 2 * kBlock) {   // two rows per thread per round, loads first
-            const int j1 = j0 + kBlock;
-            const SBMP_GAS float4* e0 = entry(j0);
-            const SBMP_GAS float4* e1 = entry(min(j1, n - 1));
-            const float4 s0 = list_load<SH>(d, e0), u0 = list_load<SH>(d, e0 + 1), s1 = list_load<SH>(d, e1),
-                         u1 = list_load<SH>(d, e1 + 1);
-            const float c0 = list_load<SH>(d, e0 + 2).x, c1 = list_load<SH>(d, e1 + 2).x;
-            put(j0, s0, u0, c0);
-            if (j1 < n) put(j1, s1, u1, c1);
+        if constexpr (SH) {
+            for (int j0 = tid; j0 < n; j0 += 2 * kBlock) {   // two rows per thread per round, loads first
+                const int j1 = j0 + kBlock;
+                const SBMP_GAS float4* e0 = entry(j0);
+                const SBMP_GAS float4* e1 = entry(min(j1, n - 1));
+                const float4 s0 = list_load<SH>(d, e0), u0 = list_load<SH>(d, e0 + 1), s1 = list_load<SH>(d, e1),
+                             u1 = list_load<SH>(d, e1 + 1);
+                const float c0 = list_load<SH>(d, e0 + 2).x, c1 = list_load<SH>(d, e1 + 2).x;
+                put(j0, s0, u0, c0);
+                if (j1 < n) put(j1, s1, u1, c1);
+            }
+        } else {
+            auto off = [&](int j) {   // byte offset of row j's list entry
+                int lo = 0;
+                for (int step = kMaxStepBlocks / 2; step > 0; step >>= 1)
+                    if (lo + step < nS && sPfx[lo + step] <= j) lo += step;
+                return list_off(d, pp, lo, j - sPfx[lo]);
+            };
+            for (int j0 = tid; j0 < n; j0 += 2 * kBlock) {   // two rows per thread per round, loads first
+                const int j1 = j0 + kBlock;
+                const int o0 = off(j0), o1 = off(min(j1, n - 1));
+                const float4 s0 = ld_sc1_f4(d.stepList, o0), u0 = ld_sc1_f4(d.stepList, o0 + 16),
+                             s1 = ld_sc1_f4(d.stepList, o1), u1 = ld_sc1_f4(d.stepList, o1 + 16);
+                const float c0 = __uint_as_float(ld_sc1_x1(d.stepList, o0 + 32)),
+                            c1 = __uint_as_float(ld_sc1_x1(d.stepList, o1 + 32));
+                put(j0, s0, u0, c0);
+                if (j1 < n) put(j1, s1, u1, c1);
+            }
         }
     }
 }
@@ -1607,12 +1792,14 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) voi
     const IterCtrl* __restrict__ ctrlPrev, const uint4* __restrict__ rngAArg, const uint2* __restrict__ rngBArg,
     const unsigned long long* __restrict__ gnewArg, const PlannerStatus* __restrict__ statusArg, long long* tlBase,
     int shRows, const int* __restrict__ shBw) {
-    // tx = t | expand << 31 and shRR = rank | ranks << 8 share the preloaded argument
-    // dwords with the prologue's first pointers (a sharded slot index needs the rank
-    // before its first load)
-    const int t = tx & 0x7fffffff, expand = (int)((unsigned)tx >> 31);
+    // tx = t | overlapped << 30 | expand << 31 and shRR = rank | ranks << 8 | arrival
+    // shards << 16 share the preloaded argument dwords with the prologue's first pointers
+    // (a sharded slot index needs the rank before its first load)
+    const int t = tx & 0x3fffffff, expand = (int)((unsigned)tx >> 31);
+    const bool ovl = !SH && ((tx >> 30) & 1);   // overlapped launches (single rank)
     const KgmtDev& d = *dp;
-    const ShardView sv{SH ? (shRR >> 8) : 1, SH ? (shRR & 0xff) : 0, SH ? shRows : 0, G(shBw)};
+    const ShardView sv{SH ? ((shRR >> 8) & 0xff) : 1, SH ? (shRR & 0xff) : 0, SH ? shRows : 0, G(shBw)};
+    if (ovl) step_wait_prev(statusArg, t, shRR >> 16);   // launch t-1 has ended, in software
     extern __shared__ float4 sDyn[];   // [LDS obstacles][prefix: nBlocks + 1 ints][R2New bits: nR2 / 32]
     __shared__ int sR1P[kMaxR1];
     __shared__ StepPlan sPlan;
@@ -1628,6 +1815,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) voi
     uint32_t* const sNew = reinterpret_cast<uint32_t*>(sPfx + (SH ? sv.nRows : d.nBlocks) + 1);
     if (blockIdx.x == 0) {
         step_planner<SH>(d, sv, t, expand, sPfx, sRed, sCovInc, sPart);
+        if (ovl) step_arrive(statusArg, t, 1 + d.nBlocks);
+        if constexpr (SH) {
+            if (expand && d.fusedX) step_planner_arrive(d, t);
+        }
         return;
     }
     float4* const sObs = sDyn;
@@ -1659,23 +1850,21 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) voi
     // The first loads' pointers are preloaded arguments; the plan's scalars and the
     // next pointers in one batch of scalar loads from the struct (one round trip, in
     // flight with the vector loads below)
-    const SBMP_GAS IterCtrl* const ctrlP = G(ctrlPrev);
-    const SBMP_GAS PlannerStatus* const statusP = G(statusArg);
-    const SBMP_GAS uint4* const rngAP = G(rngAArg);
-    const SBMP_GAS uint2* const rngBP = G(rngBArg);
-    const SBMP_GAS unsigned long long* const gnewP = G(gnewArg);
     SBMP_STAMP(0);
 
     // ---- loads that depend on nothing else (the control block as a plain load: a
     // waiting scalar load would serialise behind the scan)
-    const int4 pk = G(cnt4)[tid];
-    const IterCtrl pc = *ctrlP;
+    // (sc1 loads of everything an earlier k_step wrote: the overlapped form, step_wait_prev)
+    const int4 pk = ld_sc1_i4(cnt4, tid * 16);
+    const IterCtrl pc = ld_ctrl(ctrlPrev);
     int rowW[SH ? kMaxRanks : 1];   // sharded: the block words of this workgroup's row (its inserts)
     if constexpr (SH) row_words(sv, b, rowW);
-    const int goalIdx = statusP->goalIdx;
-    const uint4 ra = rngAP[slot];
-    const uint2 rb = rngBP[slot];
-    const unsigned long long oldWord = (lane == 0) ? gnewP[slot >> 6] : 0ull;
+    const int goalIdx = (int)ld_sc1_x1(statusArg, 0);
+    const sbmp_u32x4 ra4 = ld_sc1_x4(rngAArg, slot * 16);
+    const sbmp_u32x2 rb2 = ld_sc1_x2(rngBArg, slot * 8);
+    const uint4 ra = make_uint4(ra4[0], ra4[1], ra4[2], ra4[3]);
+    const uint2 rb = make_uint2(rb2[0], rb2[1]);
+    const unsigned long long oldWord = (lane == 0) ? ld_sc1_u64(gnewArg, (slot >> 6) * 8) : 0ull;
     asm volatile("" ::"s"(d.M), "s"(d.nBlocks), "s"(d.numIterations), "s"(d.numDisc), "s"(d.nR1), "s"(d.nR2),
                  "s"(d.cap), "s"(d.fixGNewClear), "s"(d.batchRule), "s"(d.rcpNumDisc), "s"(d.treeState),
                  "s"(d.treeCtrl), "s"(d.stepList));
@@ -1765,10 +1954,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) voi
             const int j = j0 + tid;
             const int dst = q.tsPrev + j;
             if (j < q.nIns && dst < d.M) {   // D13: the reference writes past M here
-                const SBMP_GAS float4* e = list_entry<SH>(d, pp, lo, tid);
-                const float4 s4 = list_load<SH>(d, e);
-                const float4 u4 = list_load<SH>(d, e + 1);
-                const float4 m4 = list_load<SH>(d, e + 2);
+                const int o = list_off(d, pp, lo, tid);
+                const float4 s4 = ld_sc1_f4(d.stepList, o);
+                const float4 u4 = ld_sc1_f4(d.stepList, o + 16);
+                const float4 m4 = ld_sc1_f4(d.stepList, o + 32);
                 // written through (fewer dirty lines at the boundary); the V# based at row tsPrev keeps
                 // the byte offset j * 16 far below 2^31 whatever M is
                 store_wt(d.treeState + q.tsPrev, j, s4);
@@ -1804,7 +1993,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) voi
     };
     if (!doExpand) {
         insert_prev();
-        if (lane == 0 && word != oldWord) G(d.gnewOut)[slot >> 6] = word;
+        if (lane == 0 && word != oldWord) store_wt(d.gnewOut, slot >> 6, word);
         return;
     }
 
@@ -1819,8 +2008,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) voi
     }
     g = act ? g : 0;
     const int parent = act ? q.gLo + g : 0;
-    const SBMP_GAS float4* src = G(d.treeState) + parent;   // the parent's state, and its cost
+    const SBMP_GAS float4* src = G(d.treeState) + parent;   // (sharded) the parent's state, and its cost
     const SBMP_GAS float* srcCost = &G(d.treeCtrl)[parent].w;
+    int lOff = 0;   // single rank: byte offset of the parent's list entry (fromList)
     // A parent inserted by t-1 is read from its block's compacted list: block lo with
     // sPfx[lo] <= j < sPfx[lo + 1].  j grows with the lane; when a wave's parents are
     // at most two consecutive list positions jA, jB (k >= 32 children per parent) both
@@ -1864,21 +2054,29 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) voi
                 row_words(sv, lo, w);
                 row_locate(sv, w, lo, j - sPfx[lo], &blk, &idx);
                 src = list_entry<SH>(d, pp, blk, idx);
+                srcCost = reinterpret_cast<const SBMP_GAS float*>(src + 2);
             } else {
-                src = list_entry<SH>(d, pp, lo, j - sPfx[lo]);
+                lOff = list_off(d, pp, lo, j - sPfx[lo]);
             }
-            srcCost = reinterpret_cast<const SBMP_GAS float*>(src + 2);
         }
     }
     // Parent and obstacles are issued back to back and waited for together.
     float4 p;
     float parentCost;
-    if (SH && fromList && !d.listPlain) {   // the owner's list over the mapping: system-scope loads
-        p = load_record_g(src);
-        parentCost = load_record_g(src + 2).x;
-    } else {
-        p = *src;
-        parentCost = *srcCost;
+    if constexpr (SH) {
+        if (fromList && !d.listPlain) {   // the owner's list over the mapping: system-scope loads
+            p = load_record_g(src);
+            parentCost = load_record_g(src + 2).x;
+        } else {
+            p = *src;
+            parentCost = *srcCost;
+        }
+    } else if (fromList) {   // sc1 loads (a single rank's rows and lists may be an overlapped launch's)
+        p = ld_sc1_f4(d.stepList, lOff);
+        parentCost = __uint_as_float(ld_sc1_x1(d.stepList, lOff + 32));
+    } else {   // rows [gLo, gLo + nExp): offsets g * 16 from row gLo (inactive lanes: row gLo)
+        p = ld_sc1_f4(d.treeState + q.gLo, g * 16);
+        parentCost = __uint_as_float(ld_sc1_x1(d.treeCtrl + q.gLo, g * 16 + 12));
     }
     float4 ro[kRegObs > 0 ? kRegObs : 1];
 #pragma unroll
@@ -2013,9 +2211,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) voi
     const bool flagged = (wordAll >> lane) & 1ull;
     if ((wordAll & ~__ballot(act)) != 0ull) {   // rare; keeps the wait below off the common path
         if (flagged && !act) {   // a stale flag on a slot past S: the child last written there
-            cs = G(d.uState)[slot];
-            cc = G(d.uCtrl)[slot];
-            cost = G(d.treeCtrl)[__float_as_int(cc.w)].w + cc.z;
+            cs = ld_sc1_f4(d.uState, slot * 16);
+            cc = ld_sc1_f4(d.uCtrl, slot * 16);
+            cost = __hip_atomic_load(&G(d.treeCtrl)[__float_as_int(cc.w)].w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) +
+                   cc.z;
         }
     }
     bool inGoal = false;
@@ -2112,7 +2311,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) voi
                                (c0 + c1 + c2 + c3) | ((gmin == kNoGoalIdx ? 0 : 1) << 16), __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_AGENT);
         }
-        else G(d.stepCnt)[(size_t)cp * kMaxStepBlocks + b] = cw;
+        else store_wt(d.stepCnt, cp * kMaxStepBlocks + b, cw);
     }
     SBMP_STAMP(6);
     if (tl) {
@@ -2126,6 +2325,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) voi
     };
     body();
     fx_exit();
+    if (ovl) step_arrive(statusArg, t, 1 + d.nBlocks);
 #undef SBMP_STAMP
 }
 
@@ -2196,6 +2396,44 @@ __global__ void k_seed_root(KgmtDev d, float4 rootState, float4 rootCtrl, int r1
     }
     d.status->goalIdx = kNoGoal;
     d.status->error = 0;
+}
+
+// A 64-bit digest of the replicated planning state (bench.py --gpus N checks that every
+// rank's is the same): tree rows [0, rows) (state, controls + cost,
+// parent), the five R1 tables and the R2 availability bits of parity tp, and the
+// iteration control blocks [1, iters].  Order-independent: the sum (mod 2^64) of a
+// splitmix64 of (array tag, index, 32-bit word) over every word, so grid shape and
+// atomic order do not matter.
+__device__ __forceinline__ unsigned long long hash_word(unsigned long long tag, unsigned long long i, uint32_t w) {
+    unsigned long long z = (tag << 56) ^ (i << 24) ^ (unsigned long long)w ^ (i >> 40);
+    z += 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+__global__ void k_state_hash(KgmtDev d, int rows, int tp, int iters, unsigned long long* out) {
+    unsigned long long acc = 0ull;
+    const long long stride = (long long)gridDim.x * blockDim.x;
+    const long long tid = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    for (long long i = tid; i < rows; i += stride) {
+        const float4 s4 = d.treeState[i], c4 = d.treeCtrl[i];
+        const uint32_t w[9] = {__float_as_uint(s4.x), __float_as_uint(s4.y), __float_as_uint(s4.z),
+                               __float_as_uint(s4.w), __float_as_uint(c4.x), __float_as_uint(c4.y),
+                               __float_as_uint(c4.z), __float_as_uint(c4.w), (uint32_t)d.treeParent[i]};
+        for (int k = 0; k < 9; ++k) acc += hash_word(1 + k, (unsigned long long)i, w[k]);
+    }
+    const int* tab = d.R1 + (size_t)tp * 5 * d.nR1;
+    for (long long i = tid; i < 5 * d.nR1; i += stride) acc += hash_word(16, (unsigned long long)i, (uint32_t)tab[i]);
+    const uint32_t* av = d.R2Avail + (size_t)tp * (d.nR2 / 32);
+    for (long long i = tid; i < d.nR2 / 32; i += stride) acc += hash_word(17, (unsigned long long)i, av[i]);
+    const int* cw = reinterpret_cast<const int*>(d.ctrl);
+    for (long long i = tid; i < (long long)iters * 16; i += stride)   // IterCtrl = 16 words; entries 1 .. iters
+        if ((i & 15) < 11) acc += hash_word(18, (unsigned long long)i, (uint32_t)cw[16 + i]);
+    for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off, 64);
+    if ((threadIdx.x & 63) == 0 && acc) atomicAdd(out, acc);
+}
+void launch_state_hash(const KgmtDev& d, int rows, int tp, int iters, unsigned long long* out, hipStream_t s) {
+    hipLaunchKernelGGL(k_state_hash, dim3(1024), dim3(256), 0, s, d, rows, tp, iters, out);
 }
 
 // Export helpers: reference AoS layout.
@@ -2302,7 +2540,7 @@ void launch_expand(const KgmtDev& d, int t, int agent, int blocks, int variant, 
 
 template <int AGENT, bool SH>
 static void launch_step_form(const KgmtDev& d, int t, int expand, int variant, hipStream_t s,
-                             const KernelTiming& tm) {
+                             const KernelTiming& tm, int overlap) {
     // dynamic LDS: [LDS obstacles][block prefix: nBlocks + 1 ints][R2New bits: nR2 / 32 words]
     const size_t nS = SH ? d.nBlocks / d.nranks : d.nBlocks;   // scan entries: blocks, or rows
     const size_t pfx = sizeof(int) * (nS + 1) + sizeof(uint32_t) * (size_t)(d.nR2 / 32);
@@ -2313,9 +2551,13 @@ static void launch_step_form(const KgmtDev& d, int t, int expand, int variant, h
     long long* const tlBase = (d.timeline && t == d.timelineIter && expand) ? d.timeline : nullptr;
     const int4* const cnt4 = SH ? reinterpret_cast<const int4*>(d.stepXr + d.xRowOff)
                                 : reinterpret_cast<const int4*>(d.stepCnt + (size_t)((t - 1) & 1) * kMaxStepBlocks);
-#define SBMP_STEP_ARGS                                                                                        \
-    d.devSelf, (int)((unsigned)t | ((unsigned)(expand != 0) << 31)), SH ? (d.rank | (d.nranks << 8)) : (1 << 8),  \
-        cnt4, d.ctrl + (t - 1), d.rngA, d.rngB, d.gnewOut, d.status, tlBase, SH ? d.nBlocks / d.nranks : d.nBlocks, \
+    // overlapped launches (single rank, expanding passes only): the arrival shards per launch
+    const bool ovl = !SH && overlap && expand;
+    const int shards = std::min(8, 1 + blocks);
+#define SBMP_STEP_ARGS                                                                                          \
+    d.devSelf, (int)((unsigned)t | ((unsigned)ovl << 30) | ((unsigned)(expand != 0) << 31)),                     \
+        SH ? (d.rank | (d.nranks << 8)) : ((1 << 8) | (shards << 16)), cnt4, d.ctrl + (t - 1), d.rngA, d.rngB,     \
+        d.gnewOut, d.status, tlBase, SH ? d.nBlocks / d.nranks : d.nBlocks,                                      \
         SH ? reinterpret_cast<const int*>(d.stepXr + d.xCntOff) : nullptr
     if (d.gridStart) {
         launch(k_step<AGENT, kObsGrid, SH>, grid, block, pfx + gridLds, s, tm, SBMP_STEP_ARGS);
@@ -2396,15 +2638,15 @@ int step_resident_groups(const KgmtDev& d, int agent, int variant, StepResidency
 
 template <int AGENT>
 static void launch_step_agent(const KgmtDev& d, int t, int expand, int variant, hipStream_t s,
-                              const KernelTiming& tm) {
-    if (d.sharded) launch_step_form<AGENT, true>(d, t, expand, variant, s, tm);
-    else launch_step_form<AGENT, false>(d, t, expand, variant, s, tm);
+                              const KernelTiming& tm, int overlap) {
+    if (d.sharded) launch_step_form<AGENT, true>(d, t, expand, variant, s, tm, overlap);
+    else launch_step_form<AGENT, false>(d, t, expand, variant, s, tm, overlap);
 }
 
 void launch_step(const KgmtDev& d, int t, int expand, int agent, int variant, hipStream_t s,
-                 const KernelTiming& tm) {
-    if (agent == 0) launch_step_agent<0>(d, t, expand, variant, s, tm);
-    else launch_step_agent<1>(d, t, expand, variant, s, tm);
+                 const KernelTiming& tm, int overlap) {
+    if (agent == 0) launch_step_agent<0>(d, t, expand, variant, s, tm, overlap);
+    else launch_step_agent<1>(d, t, expand, variant, s, tm, overlap);
 }
 
 void launch_fold_r2(const KgmtDev& d, int tFirst, int tLast, hipStream_t s, const KernelTiming& tm) {

@@ -23,8 +23,11 @@ void launch_expand(const KgmtDev& d, int t, int agent, int blocks, int variant, 
                    const KernelTiming& tm = KernelTiming());
 // k_fold_r2: add the key log of iterations [tFirst, tLast] (at most kFoldEvery) to R2Valid / R2Invalid.
 // k_step(t): one launch per iteration on a single rank; expand == 0: flush pass.
+// overlap (single rank, expanding passes): the launch waits in-kernel for every workgroup
+// of k_step(t-1), which may still run on another stream, and reports its own arrivals
+// (DESIGN.md §5.6); the counters are zeroed at begin().
 void launch_step(const KgmtDev& d, int t, int expand, int agent, int variant, hipStream_t s,
-                 const KernelTiming& tm = KernelTiming());
+                 const KernelTiming& tm = KernelTiming(), int overlap = 0);
 // Workgroups of the k_step form launch_step would pick for d that the device holds at
 // once (occupancy per CU x CUs); k_step needs all of its 1 + blocks resident, since
 // its expanders wait for workgroup 0.  0 if the query fails.
@@ -44,6 +47,18 @@ void launch_pack(const KgmtDev& d, int t, int blocks, hipStream_t s, const Kerne
 // rank q's, oneshot_inbox_words() u64 each, zeroed once); seq = this exchange's number
 // in the plan's lifetime (1, 2, ...), the same on every rank.
 size_t oneshot_inbox_words(long long n, int nranks);
+// The list mirror's start-up check (kgmt_kernels.hip, KgmtPlanner::mirror_self_test):
+// phase 0 touches this rank's probed entries with plain loads, 1 pushes this rank's
+// pattern of `pass` into every rank's mirror (system scope), 2 checks them (plain loads;
+// mismatching float4 words are added to *bad).
+struct MirrorProbe {
+    float4* peer[kMaxRanks];   // every rank's mirror, mapped here
+    const float4* own;         // this rank's
+    int nranks, rank, nBlocks;   // mirror layout [2][nBlocks][kBlock][kStepEntry]
+    int blocks, entries;       // probed: global blocks < blocks, entries < entries, both parities
+    int* bad;
+};
+void launch_mirror_probe(const MirrorProbe& a, int phase, int pass, float* sink, hipStream_t s);
 // error: the planner's status word (set to kErrExchange when a peer never arrives).
 // compact (sharded k_step): the send layout, sent in compact form (kgmt_kernels.hip).
 struct OneshotLayout {
@@ -71,6 +86,9 @@ void launch_solution_path(const KgmtDev& d, int node, int maxDepth, int* out, in
                           hipStream_t s);
 void launch_seed_root(const KgmtDev& d, float4 rs, float4 rc, int r1, int r2, hipStream_t s);
 void launch_export_tree(const KgmtDev& d, float* samples, float* costs, hipStream_t s);
+// *out += the digest of tree rows [0, rows), the tables of parity tp and ctrl[1 .. iters]
+// (k_state_hash; *out zeroed by the caller).
+void launch_state_hash(const KgmtDev& d, int rows, int tp, int iters, unsigned long long* out, hipStream_t s);
 void launch_export_unexplored(const KgmtDev& d, float* samples, int* uParent, hipStream_t s);
 
 // xorwow_jump.cpp: cuRAND seeding and the subsequence jump matrices.

@@ -87,6 +87,8 @@ static float markstein_rcp(float b) {
         throw Error(SBMP_ERR_COMM, "k_oneshot: a peer rank's exchange flag did not arrive within 20 s");
     if (e == kErrStepHandoff)
         throw Error(SBMP_ERR_HIP, "k_step: the planner workgroup's hand-off did not arrive within 1 s");
+    if (e == kErrStepOverlap)
+        throw Error(SBMP_ERR_HIP, "overlapped k_step: the previous launch's workgroups did not all arrive within 1 s");
     throw Error(SBMP_ERR_HIP, "in-kernel wait failed (status " + std::to_string(e) + ")");
 }
 
@@ -118,6 +120,12 @@ KgmtPlanner::KgmtPlanner(const sbmp_kgmt_params& p, int nranks, int rank, Exchan
     } else {
         SBMP_HIP(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
     }
+    if (!shared && nranks == 1 && !ex) {   // a single rank: the overlapped k_step's second stream (§5.6)
+        SBMP_HIP(hipStreamCreateWithFlags(&stream2_, hipStreamNonBlocking));
+        SBMP_HIP(hipEventCreateWithFlags(&evFork_, hipEventDisableTiming));
+        SBMP_HIP(hipEventCreateWithFlags(&evJoin_, hipEventDisableTiming));
+    }
+    if (const char* v = getenv("SBMP_OVERLAP")) overlapReq_ = atoi(v) ? 1 : 0;
     // Obstacle-list form of k_expand (diagnostics / A-B): 0 auto, 1 LDS, 2 LDS x4,
     // 3 registers, 4 grid index at any count, 5 global list without the grid.
     if (const char* v = getenv("SBMP_EXPAND_VARIANT")) expandVariant_ = std::min(5, std::max(0, atoi(v)));
@@ -284,7 +292,10 @@ KgmtPlanner::KgmtPlanner(const sbmp_kgmt_params& p, int nranks, int rank, Exchan
     d.logSlots = expandBlocks_ * kBlock;
     d.r2log = (d.nR2 <= kLogMaxR2) ? alloc<uint16_t>((size_t)kFoldEvery * d.logSlots) : nullptr;
     d.ctrl = alloc<IterCtrl>(p.numIterations + 2);
-    d.status = alloc<PlannerStatus>(1);
+    // the status block, then the overlapped k_step's arrival counters (kDoneWordOff)
+    static_assert(sizeof(PlannerStatus) <= kDoneWordOff * sizeof(unsigned), "counters behind the status block");
+    d.status = reinterpret_cast<PlannerStatus*>(alloc<unsigned>(kStatusWords));
+    SBMP_HIP(hipMemset(d.status, 0, sizeof(unsigned) * kStatusWords));
     SBMP_HIP(hipHostMalloc(reinterpret_cast<void**>(&poll_), sizeof(PollBuf), hipHostMallocDefault));
     d.timeline = nullptr;
     d.timelineFin = nullptr;
@@ -327,7 +338,8 @@ KgmtPlanner::KgmtPlanner(const sbmp_kgmt_params& p, int nranks, int rank, Exchan
             ex_->share_buffer(own, sizeof(unsigned long long) * words, ib);
             for (int q = 0; q < nranks; ++q) inbox_[q] = static_cast<unsigned long long*>(ib[q]);
             oneshot_ = true;
-            if (!oneshot_self_test()) {
+            oneshotCheck_ = oneshot_self_test() ? 1 : -1;
+            if (oneshotCheck_ < 0) {
                 oneshot_ = false;   // on every rank: the verdict is all-reduced
                 fprintf(stderr, "sbmp: rank %d: the one-shot exchange failed its start-up check on this machine; "
                                 "the per-iteration exchange is the communicator's all-reduce\n", rank);
@@ -352,6 +364,18 @@ KgmtPlanner::KgmtPlanner(const sbmp_kgmt_params& p, int nranks, int rank, Exchan
             for (int q = 0; q < nranks; ++q) d.mirrorPeer[q] = static_cast<float4*>(mp[q]);
             d.stepMirror = own;
             d.listPlain = 1;
+            // The mirror relies on the kernel boundary dropping this GPU's cached lines of
+            // entries a peer rewrote over xGMI: checked once here, on this machine (every
+            // rank gets the same all-reduced verdict); on failure every rank reads the lists
+            // from the owners' record buffers with system-scope loads instead (SBMP_MIRROR=0).
+            mirrorCheck_ = mirror_self_test() ? 1 : -1;
+            if (mirrorCheck_ < 0) {
+                d.stepMirror = nullptr;
+                for (int q = 0; q < kMaxRanks; ++q) d.mirrorPeer[q] = nullptr;
+                d.listPlain = 0;
+                fprintf(stderr, "sbmp: rank %d: the list mirror failed its start-up check on this machine; k_step "
+                                "reads the peers' lists over the mapping (system-scope loads)\n", rank);
+            }
         }
         // The fused exchange (k_step_exchange, kgmt_kernels.hip): with the mirror and the
         // compact form, the last expanding workgroup of k_step runs the exchange, and no
@@ -429,11 +453,56 @@ bool KgmtPlanner::oneshot_self_test() {
     return anyBad == 0;
 }
 
+// The list mirror checked once on this machine (the kernels and their
+// sequence: k_mirror_touch / push / check, kgmt_kernels.hip).  Probed: both parities, the
+// first 64 entries of the first min(nBlocks, 64) global blocks (every rank's among them),
+// two passes.  SBMP_MIRROR_SELFTEST=fail makes this rank report a failure (tests).
+bool KgmtPlanner::mirror_self_test() {
+    MirrorProbe a{};
+    for (int q = 0; q < d_.nranks; ++q) a.peer[q] = d_.mirrorPeer[q];
+    a.own = d_.stepMirror;
+    a.nranks = d_.nranks;
+    a.rank = d_.rank;
+    a.nBlocks = d_.nBlocks;
+    a.blocks = std::min(d_.nBlocks, 64);
+    a.entries = 64;
+    int* dev = alloc<int>(2);   // [bad, sink]
+    a.bad = dev;
+    unsigned long long* verdict = alloc<unsigned long long>(2);
+    SBMP_HIP(hipMemsetAsync(dev, 0, sizeof(int) * 2, stream_));
+    for (int pass = 0; pass < 2; ++pass) {
+        launch_mirror_probe(a, 0, pass, reinterpret_cast<float*>(dev + 1), stream_);   // lines of the old values cached
+        ex_->barrier(stream_);
+        launch_mirror_probe(a, 1, pass, nullptr, stream_);   // every rank pushes into every mirror
+        ex_->barrier(stream_);                                // every push has completed (stream drained)
+        launch_mirror_probe(a, 2, pass, nullptr, stream_);   // a new launch reads them with plain loads
+    }
+    SBMP_HIP(hipGetLastError());
+    int bad = 0;
+    SBMP_HIP(hipMemcpyAsync(&bad, dev, sizeof(int), hipMemcpyDeviceToHost, stream_));
+    SBMP_HIP(hipStreamSynchronize(stream_));
+    bool ok = bad == 0;
+    if (!ok) fprintf(stderr, "sbmp: rank %d: list mirror check: %d stale or wrong words\n", d_.rank, bad);
+    if (const char* f = getenv("SBMP_MIRROR_SELFTEST"))   // tests: this rank reports a failure
+        if (std::string(f) == "fail") ok = false;
+    const unsigned long long badv = ok ? 0ull : 1ull;
+    SBMP_HIP(hipMemcpyAsync(verdict, &badv, sizeof(badv), hipMemcpyHostToDevice, stream_));
+    ex_->allreduce_u64(verdict, verdict + 1, 1, stream_);
+    unsigned long long anyBad = 0;
+    SBMP_HIP(hipMemcpyAsync(&anyBad, verdict + 1, sizeof(anyBad), hipMemcpyDeviceToHost, stream_));
+    SBMP_HIP(hipStreamSynchronize(stream_));
+    return anyBad == 0;
+}
+
 KgmtPlanner::~KgmtPlanner() {
     if (stream_) {
         (void)hipSetDevice(p_.device);
+        if (stream2_) (void)hipStreamSynchronize(stream2_);
         (void)hipStreamSynchronize(stream_);
     }
+    if (stream2_) (void)hipStreamDestroy(stream2_);
+    if (evFork_) (void)hipEventDestroy(evFork_);
+    if (evJoin_) (void)hipEventDestroy(evJoin_);
     for (auto& q : pending_) {
         (void)hipEventDestroy(q.a);
         (void)hipEventDestroy(q.b);
@@ -457,6 +526,7 @@ void KgmtPlanner::begin(const float* initial, const float* goal, const float* d_
         if (!std::isfinite(initial[i]))
             throw Error(SBMP_ERR_INVALID_ARGUMENT, "initial state (x, y, theta, v) must be finite");
     SBMP_HIP(hipSetDevice(p_.device));
+    join_streams();   // a previous plan's launches on the second stream come first
     KgmtDev& d = d_;
     hipStream_t s = stream_;
     // Constructor state (KGMT.cu:16-72): zero-filled vectors, parents -1, R1Score 1.0.
@@ -484,6 +554,9 @@ void KgmtPlanner::begin(const float* initial, const float* goal, const float* d_
     SBMP_HIP(hipMemsetAsync(d.R2Invalid, 0, sizeof(int) * d.nR2, s));
     launch_fill_f32(d.R1Score, 1.0f, 2 * d.nR1, s);
     SBMP_HIP(hipMemsetAsync(d.ctrl, 0, sizeof(IterCtrl) * (p_.numIterations + 2), s));
+    // the overlapped k_step's arrival counters count the launches of this plan
+    SBMP_HIP(hipMemsetAsync(reinterpret_cast<unsigned*>(d.status) + kDoneWordOff, 0,
+                            sizeof(unsigned) * (kStatusWords - kDoneWordOff), s));
 
     // Obstacles: a private float4 copy of the caller's device array (KGMT.cu:80 takes
     // d_obstacles by pointer; copying keeps the row layout 16-B aligned).
@@ -529,6 +602,9 @@ void KgmtPlanner::begin(const float* initial, const float* goal, const float* d_
     t_next_ = 1;
     lastFolded_ = 0;
     begun_ = true;
+    // overlapped launches: one rank in the k_step form, when asked (SBMP_OVERLAP=1 / sbmp_kgmt_set_overlap)
+    overlap_ = stream2_ && d.stepMode && !d.sharded && overlapReq_ != 0;
+    ovlRun_ = ovlNextAlt_ = ovlAltUsed_ = false;
     wallMs_ = 0.0;
     SBMP_HIP(hipStreamSynchronize(s));
     if (ex_) ex_->barrier(s);   // every rank set up before the first (time-bounded) exchange
@@ -596,6 +672,9 @@ void KgmtPlanner::path_info(sbmp_path_info* out) {
     out->commRanks = ex_ ? ex_->comm_ranks() : 0;
     out->listMirror = d.stepMirror ? 1 : 0;
     out->fusedExchange = d.fusedX ? 1 : 0;
+    out->overlap = overlap_ ? 1 : 0;
+    out->oneshotCheck = oneshotCheck_;
+    out->mirrorCheck = mirrorCheck_;
 }
 
 void KgmtPlanner::build_grid(const float* d_obstacles, int nObs) {
@@ -673,8 +752,40 @@ void KgmtPlanner::stage_pack(int t) {
 
 void KgmtPlanner::stage_step(int t) {
     upload_dev();
-    launch_step(d_, t, 1, p_.agent, expandVariant_, stream_, timing(K_STEP));
+    launch_step(d_, t, 1, p_.agent, expandVariant_, step_stream(), timing(K_STEP), overlap_ ? 1 : 0);
     flushed_ = false;
+}
+
+// The stream of the next k_step launch.  Overlapped: the first launch after a join goes on
+// stream_, and stream2_ is forked from the point just before it, so that stream2_'s next
+// launch waits for everything before that launch and for nothing after it; from then on
+// the launches alternate.  A launch on one stream thus follows the launch two iterations
+// back (its stream predecessor) and whatever preceded the last join; it waits for the
+// launch just before it inside the kernel (step_wait_prev).
+hipStream_t KgmtPlanner::step_stream() {
+    if (!overlap_) return stream_;
+    if (!ovlRun_) {
+        SBMP_HIP(hipEventRecord(evFork_, stream_));
+        SBMP_HIP(hipStreamWaitEvent(stream2_, evFork_, 0));
+        ovlRun_ = true;
+        ovlNextAlt_ = true;
+        return stream_;
+    }
+    const bool alt = ovlNextAlt_;
+    ovlNextAlt_ = !ovlNextAlt_;
+    if (alt) ovlAltUsed_ = true;
+    return alt ? stream2_ : stream_;
+}
+
+// stream_ waits for what was enqueued on stream2_; anything other than an overlapped
+// k_step launch is enqueued on stream_ after this.
+void KgmtPlanner::join_streams() {
+    if (!ovlRun_) return;
+    if (ovlAltUsed_) {
+        SBMP_HIP(hipEventRecord(evJoin_, stream2_));
+        SBMP_HIP(hipStreamWaitEvent(stream_, evJoin_, 0));
+    }
+    ovlRun_ = ovlNextAlt_ = ovlAltUsed_ = false;
 }
 
 void KgmtPlanner::stage_exchange(int t) {
@@ -711,6 +822,7 @@ void KgmtPlanner::stage_exchange(int t) {
 
 // k_step mode: complete the last enqueued iteration (insert it, plan t_next) before a read-back
 void KgmtPlanner::flush() {
+    join_streams();
     if (d_.stepMode && begun_ && !flushed_) {
         upload_dev();
         launch_step(d_, t_next_, 0, p_.agent, expandVariant_, stream_, KernelTiming());
@@ -731,6 +843,7 @@ void KgmtPlanner::stage_fold(int t) {
 // Bring R2Valid / R2Invalid up to iteration tLast (k_fold_r2 over the key log).
 void KgmtPlanner::fold_to(int tLast) {
     if (tLast <= lastFolded_) return;
+    join_streams();
     if (d_.r2log) launch_fold_r2(d_, lastFolded_ + 1, tLast, stream_, timing(K_FOLD));
     lastFolded_ = tLast;
 }
@@ -740,6 +853,7 @@ void KgmtPlanner::fold_to(int tLast) {
 void KgmtPlanner::upload_dev() {
     if (!dDev_) throw Error(SBMP_ERR_STATE, "k_step: the plan struct has no device copy");
     if (uploaded_ && std::memcmp(&d_, dStage_, sizeof(KgmtDev)) == 0) return;
+    join_streams();   // the copy goes on stream_, behind every launch that reads the old one
     if (uploaded_) SBMP_HIP(hipStreamSynchronize(stream_));   // the previous copy has been read
     std::memcpy(dStage_, &d_, sizeof(KgmtDev));
     SBMP_HIP(hipMemcpyAsync(dDev_, dStage_, sizeof(KgmtDev), hipMemcpyHostToDevice, stream_));
@@ -747,7 +861,7 @@ void KgmtPlanner::upload_dev() {
 }
 
 void KgmtPlanner::sync() {
-    flush();
+    flush();   // joins the second stream first
     SBMP_HIP(hipStreamSynchronize(stream_));
     wallMs_ = now_ms() - t0_;
     if (d_.timeline && !timelineDumped_ && t_next_ > d_.timelineIter) {
@@ -887,6 +1001,27 @@ void KgmtPlanner::copy_tree(float* samples, int* parent, float* costs) {
     SBMP_HIP(hipStreamSynchronize(stream_));
     (void)hipFree(dS);
     (void)hipFree(dC);
+}
+
+// The replicated state's digest (k_state_hash): every rank of a sharded run holds the same
+// tree, tables and control blocks, so every rank's digest must be the same.
+unsigned long long KgmtPlanner::state_hash() {
+    sbmp_plan_result r;
+    result(&r);   // syncs (the flush pass has inserted the last iteration)
+    unsigned long long* dev = alloc_scratch_u64();
+    SBMP_HIP(hipMemsetAsync(dev, 0, sizeof(unsigned long long), stream_));
+    const int rows = std::min(std::max(r.treeSize, 1), d_.M);
+    const int tp = d_.stepMode ? (t_next_ & 1) : 0;   // the tables of iteration t_next (copy_regions' parity)
+    launch_state_hash(d_, rows, tp, r.iterations, dev, stream_);
+    unsigned long long h = 0;
+    SBMP_HIP(hipMemcpyAsync(&h, dev, sizeof(h), hipMemcpyDeviceToHost, stream_));
+    SBMP_HIP(hipStreamSynchronize(stream_));
+    return h;
+}
+
+unsigned long long* KgmtPlanner::alloc_scratch_u64() {
+    if (!scratch_) scratch_ = alloc<unsigned long long>(8);
+    return scratch_;
 }
 
 int KgmtPlanner::solution_path(int node, int* rows, float* samples, float* costs, int capacity) {

@@ -76,6 +76,9 @@ public:
     // Rows root .. node (node < 0: the solution node); returns the length (0: no
     // solution).  Outputs may be null; capacity in rows (too small: SBMP_ERR_INVALID_ARGUMENT).
     virtual int solution_path(int node, int* rows, float* samples, float* costs, int capacity) = 0;
+    // Digest of the replicated state (tree rows, region tables, control blocks): the same on
+    // every rank of a sharded run (k_state_hash).
+    virtual unsigned long long state_hash() = 0;
     void export_csv(const std::string& dir);
 
     virtual std::vector<sbmp_kernel_stat> kernel_stats() = 0;
@@ -83,6 +86,7 @@ public:
     virtual void reset_kernel_stats() = 0;
     virtual void set_profiling(bool on) = 0;
     virtual void enqueue_delay(double us) = 0;
+    virtual void set_overlap(int) {}   // overlapped k_step launches from the next begin() (single rank)
     virtual std::vector<float> kernel_samples(const std::string& name) = 0;
 
 protected:
@@ -129,12 +133,17 @@ public:
     void copy_rng(uint32_t* states) override;
     std::vector<sbmp_iter_record> iter_log() override;
     int solution_path(int node, int* rows, float* samples, float* costs, int capacity) override;
+    unsigned long long state_hash() override;
 
     std::vector<sbmp_kernel_stat> kernel_stats() override;
     void path_info(sbmp_path_info* out) override;
     void reset_kernel_stats() override;
     void set_profiling(bool on) override { p_.profileKernels = on ? 1 : 0; }
-    void enqueue_delay(double us) override { launch_delay(us, stream_); }
+    void enqueue_delay(double us) override {
+        join_streams();
+        launch_delay(us, stream_);
+    }
+    void set_overlap(int on) override { overlapReq_ = on ? 1 : 0; }   // from the next begin()
     std::vector<float> kernel_samples(const std::string& name) override;
 
     // ---- stages of one iteration (enqueue() composes them; a LocalShardGroup
@@ -175,6 +184,20 @@ private:
     void upload_dev();
     hipStream_t stream_ = nullptr;
     bool ownStream_ = true;
+    // Overlapped k_step launches (single rank): consecutive iterations
+    // alternate between stream_ and stream2_ with no stream dependency; k_step(t) waits
+    // in-kernel for k_step(t-1).  Anything else enqueued (fold, flush, copies) first joins
+    // stream2_ into stream_ (join_streams); the first launch after a join goes on stream_
+    // and forks stream2_ from the point just before it.
+    hipStream_t stream2_ = nullptr;
+    hipEvent_t evFork_ = nullptr, evJoin_ = nullptr;
+    int overlapReq_ = 0;       // sbmp_kgmt_set_overlap / SBMP_OVERLAP=1 (off by default: §5.6 measures it slower)
+    bool overlap_ = false;     // this plan launches overlapped (decided at begin())
+    bool ovlRun_ = false;      // launches since the last join alternate
+    bool ovlNextAlt_ = false;  // the next launch goes on stream2_
+    bool ovlAltUsed_ = false;  // stream2_ holds launches stream_ has not joined
+    void join_streams();
+    hipStream_t step_stream();
     Exchange* ex_ = nullptr;
     int t_next_ = 1;
     bool begun_ = false;
@@ -204,8 +227,10 @@ private:
     size_t xWords_ = 0;
     bool oneshot_ = false;                   // sharded: the exchange is k_oneshot over IPC-mapped inboxes
     bool oneshot_self_test();                // k_oneshot checked once at construction (all ranks agree)
+    bool mirror_self_test();                 // the list mirror checked once at construction (all ranks agree)
+    int oneshotCheck_ = 0, mirrorCheck_ = 0;   // start-up checks: 0 not run, 1 passed, -1 failed (fell back)
     unsigned long long* inbox_[kMaxRanks] = {nullptr};
-    bool compactX_ = true;   // sharded k_step: k_oneshot sends the compact form of the exchange   // every rank's list mirror (sharded k_step, one-shot)
+    bool compactX_ = true;   // sharded k_step: k_oneshot sends the compact form of the exchange
     unsigned long long xSeq_ = 0;            // exchanges so far (the same count on every rank)
     uint32_t* jumps_ = nullptr;
     float4* obs_ = nullptr;
@@ -215,6 +240,8 @@ private:
     float4* gridBoxes_ = nullptr;
     size_t gridBoxesCap_ = 0;
     std::vector<void*> allocs_;
+    unsigned long long* scratch_ = nullptr;   // 8 device words for small results (state_hash)
+    unsigned long long* alloc_scratch_u64();
     double wallMs_ = 0.0;
     double t0_ = 0.0;
 
@@ -267,6 +294,7 @@ public:
     int solution_path(int node, int* rows, float* samples, float* costs, int capacity) override {
         return r0().solution_path(node, rows, samples, costs, capacity);   // every rank holds the whole tree
     }
+    unsigned long long state_hash() override;   // every rank's digest; throws if they differ
 
     std::vector<sbmp_kernel_stat> kernel_stats() override { return r0().kernel_stats(); }
     void path_info(sbmp_path_info* out) override { r0().path_info(out); }

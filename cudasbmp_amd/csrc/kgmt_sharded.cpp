@@ -262,6 +262,15 @@ void LocalShardGroup::copy_unexplored(float* samples, int* uParent) {
     }
 }
 
+unsigned long long LocalShardGroup::state_hash() {
+    sync();
+    const unsigned long long h = ranks_[0]->state_hash();
+    for (size_t q = 1; q < ranks_.size(); ++q)
+        if (ranks_[q]->state_hash() != h)
+            throw Error(SBMP_ERR_STATE, "local shard group: rank " + std::to_string(q) + "'s replicated state differs");
+    return h;
+}
+
 void LocalShardGroup::copy_rng(uint32_t* states) {
     const int n = num_slots(), P = (int)ranks_.size();
     std::vector<uint32_t> st((size_t)n * 6);

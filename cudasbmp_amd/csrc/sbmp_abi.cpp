@@ -409,6 +409,21 @@ sbmp_status sbmp_kgmt_set_profiling(sbmp_kgmt* h, int enabled) {
     });
 }
 
+sbmp_status sbmp_kgmt_state_hash(sbmp_kgmt* h, uint64_t* out) {
+    return guarded([&] {
+        PLANNER(h);
+        REQUIRE(out, "out must be non-NULL");
+        *out = (uint64_t)P.state_hash();
+    });
+}
+
+sbmp_status sbmp_kgmt_set_overlap(sbmp_kgmt* h, int enabled) {
+    return guarded([&] {
+        PLANNER(h);
+        P.set_overlap(enabled != 0);
+    });
+}
+
 // readObstaclesFromCSV (reference src/helper/helper.cu:11-34): values separated
 // by whitespace or single commas, read line by line with operator>>.
 sbmp_status sbmp_read_obstacles_csv(const char* path, int workspaceDim, float* out, int capacity,

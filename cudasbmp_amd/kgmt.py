@@ -333,7 +333,10 @@ class KGMT:
                 "resident_groups": pi.residentGroups, "needed_groups": pi.neededGroups,
                 "exchange": self.EXCHANGES[pi.exchange] if 0 <= pi.exchange < 3 else pi.exchange,
                 "nranks": pi.nranks, "rank": pi.rank, "rccl_nranks": pi.commRanks,
-                "list_mirror": bool(pi.listMirror), "fused_exchange": bool(pi.fusedExchange)}
+                "list_mirror": bool(pi.listMirror), "fused_exchange": bool(pi.fusedExchange),
+                "overlap": bool(pi.overlap),
+                "oneshot_check": {0: "not run", 1: "passed", -1: "failed"}.get(pi.oneshotCheck, pi.oneshotCheck),
+                "mirror_check": {0: "not run", 1: "passed", -1: "failed"}.get(pi.mirrorCheck, pi.mirrorCheck)}
 
     def kernel_samples(self, name: str) -> np.ndarray:
         """Per-launch durations (ms) of kernel `name` since the last reset_kernel_stats()."""
@@ -350,3 +353,13 @@ class KGMT:
 
     def set_profiling(self, enabled: bool) -> None:
         nat.call("sbmp_kgmt_set_profiling", self._h, int(bool(enabled)))
+
+    def state_hash(self) -> int:
+        """64-bit digest of the replicated state (tree, tables, control blocks): equal on every rank."""
+        h = ctypes.c_uint64()
+        nat.call("sbmp_kgmt_state_hash", self._h, ctypes.byref(h))
+        return int(h.value)
+
+    def set_overlap(self, enabled: bool) -> None:
+        """Overlapped k_step launches (one rank; on by default) from the next begin() / plan()."""
+        nat.call("sbmp_kgmt_set_overlap", self._h, int(bool(enabled)))

@@ -32,12 +32,14 @@ pytestmark = pytest.mark.gpu
 BENCH_SEED = 20240807
 
 
-def _run(kw, seed, obs, P=0, threads=16):
+def _run(kw, seed, obs, P=0, threads=16, overlap=None):
     from cudasbmp_amd import KGMT, DeviceBuffer
     cfg = dict(DEMO)
     extra = {k: kw[k] for k in ("samplesPerIteration", "agent", "fixGNewClear", "batchRule") if k in kw}
     cfg.update({k: v for k, v in kw.items() if k not in extra})
     g = KGMT(**cfg, **extra, _local_group=P)
+    if overlap is not None:
+        g.set_overlap(overlap)
     r = g.plan(DEMO_INITIAL, DEMO_GOAL, DeviceBuffer(obs), len(obs), seed=seed)
     o = _oracle(cfg, extra, threads=threads)
     o.plan(DEMO_INITIAL, DEMO_GOAL, obs, seed)
@@ -73,8 +75,14 @@ def test_c1_as_configured_bit_exact(oracle_lib):
     assert_same_state(g, o, label="c1 as configured")
 
 
-def test_c3_bench_mode_bit_exact(obstacles, oracle_lib):
-    g, o, r = _run(_bench_kw(262144, 72), BENCH_SEED, obstacles)
+@pytest.mark.parametrize("overlap", [True, False], ids=["overlapped", "serial"])
+def test_c3_bench_mode_bit_exact(obstacles, oracle_lib, overlap):
+    """Both launch forms of one rank: overlapped k_step launches on two streams, each
+    waiting in-kernel for the previous one (the default), and one
+    stream with a kernel boundary per iteration."""
+    g, o, r = _run(_bench_kw(262144, 72), BENCH_SEED, obstacles, overlap=overlap)
+    info = g.path_info()
+    assert info["form"] == "k_step" and info["overlap"] == overlap, info
     log = g.iter_log()
     assert r.iterations == 72 and log[5:, 5].min() > 250000
     assert (log[20:, 6] <= 4096).all(), "steady state: the planner workgroup inserts"
@@ -152,3 +160,19 @@ def test_c3_path_info_is_k_step():
     info = g.path_info()
     assert info["form"] == "k_step" and info["obstacle_form"] == "registers" and info["exchange"] == "none", info
     assert info["resident_groups"] >= info["needed_groups"] == 1025, info
+
+
+@pytest.mark.parametrize("P", [2, 8])
+def test_c5_sharded_per_rank_shape_bit_exact(P, oracle_lib):
+    """The kernel every rank of the 8-GPU c5 configuration runs (BASELINE.json c5: 1,048,576
+    children per iteration over 8 GPUs = 131,072 per rank on the 10,000-box field): the
+    sharded k_step with the uniform-grid obstacle index, here as a local shard group of P
+    ranks of 131,072 children each on one GPU, 6 iterations, whole state bit-exact.
+    Reference: collisionCheck.cu:16-28 (the per-step box loop), KGMT.cu:341-414."""
+    obs = _c5_obstacles()
+    g, o, r = _run(_bench_kw(131072 * P, 6, maxTreeSize=1 << 25), BENCH_SEED, obs, P=P)
+    info = g.path_info()
+    assert info["form"] == "k_step" and info["obstacle_form"] == "grid" and info["nranks"] == P, info
+    assert info["needed_groups"] == 1 + 512 and info["resident_groups"] >= info["needed_groups"], info
+    assert r.iterations == 6 and g.iter_log()[:, 5].max() == 131072 * P
+    assert_same_state(g, o, label=f"c5 per-rank shape, {P} ranks")

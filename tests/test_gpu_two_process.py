@@ -57,6 +57,10 @@ def _rank_main(rank, port, kw, seed, out_dir, exchange, delay=0.0):
         os.environ["SBMP_ONESHOT_SELFTEST"] = "fail"
     else:
         os.environ.pop("SBMP_ONESHOT_SELFTEST", None)
+    if exchange == "mirror-check-fails" and rank == 1:   # only rank 1's list-mirror check "fails"
+        os.environ["SBMP_MIRROR_SELFTEST"] = "fail"
+    else:
+        os.environ.pop("SBMP_MIRROR_SELFTEST", None)
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     import torch.distributed as dist
@@ -76,6 +80,8 @@ def _rank_main(rank, port, kw, seed, out_dir, exchange, delay=0.0):
     oneshots = g.kernel_stats().get("k_oneshot", (0, 0.0))[0]
     pinfo = g.path_info()
     mirror, fused = pinfo["list_mirror"], pinfo["fused_exchange"]
+    checks = np.array([pinfo["oneshot_check"], pinfo["mirror_check"]])
+    digest = np.uint64(g.state_hash())   # the replicated state: the same on both ranks
     s, p, c = g.tree()
     G, GN = g.flags()          # GNew words live with their owner: merged by the all-reduce
     reg = g.regions()          # R2Valid / R2Invalid: each rank folded its own children
@@ -83,6 +89,7 @@ def _rank_main(rank, port, kw, seed, out_dir, exchange, delay=0.0):
     rng = g.rng()
     np.savez(os.path.join(out_dir, f"rank{rank}.npz"), s=s, p=p, c=c, G=G, GN=GN, u=u, up=up, rng=rng,
              log=g.iter_log(), res=np.array([r.iterations, r.treeSize, r.goalIndex]), oneshots=oneshots, mirror=mirror, fused=fused,
+             checks=checks, digest=digest,
              cost=np.float32(r.costToGoal), **{"reg_" + k: v for k, v in reg.items()})
     g.close()
     dist.destroy_process_group()
@@ -108,6 +115,10 @@ def _rank_main(rank, port, kw, seed, out_dir, exchange, delay=0.0):
     # all-reduce together (one rank alone would leave the other waiting for its flags)
     (dict(samplesPerIteration=4096, batchRule="fill", maxTreeSize=200000, numIterations=15, goalThreshold=0.0), 21,
      "oneshot-check-fails", 0.0),
+    # rank 1's start-up check of the list mirror fails: both ranks must drop the mirror (and with
+    # it the fused exchange) together and read the lists over the mapping with k_oneshot
+    (dict(samplesPerIteration=4096, batchRule="fill", maxTreeSize=200000, numIterations=15, goalThreshold=0.0), 21,
+     "mirror-check-fails", 0.0),
 ])
 def test_two_processes_one_gpu_bit_exact(kw, seed, exchange, delay, tmp_path, obstacles, oracle_lib):
     ctx = mp.get_context("spawn")
@@ -145,10 +156,16 @@ def test_two_processes_one_gpu_bit_exact(kw, seed, exchange, delay, tmp_path, ob
         assert bool(d["fused"]) == fused, f"rank {r}: fused exchange {bool(d['fused'])}"
         assert bool(d["mirror"]) == (exchange in ("oneshot", "oneshot-kernel")), \
             f"rank {r}: list mirror {bool(d['mirror'])}"
-        if exchange in ("oneshot-kernel", "oneshot-remote"):
+        if exchange in ("oneshot-kernel", "oneshot-remote", "mirror-check-fails"):
             assert int(d["oneshots"]) > 0, f"rank {r}: the one-shot exchange did not run"
         else:
             assert int(d["oneshots"]) == 0, f"rank {r}: k_oneshot ran ({int(d['oneshots'])} launches)"
+        # the start-up checks: which ran, and the all-reduced verdict every rank acted on
+        want = {"collective": ["not run", "not run"], "oneshot-check-fails": ["failed", "not run"],
+                "oneshot-remote": ["passed", "not run"], "mirror-check-fails": ["passed", "failed"]}.get(
+                    exchange, ["passed", "passed"])
+        assert d["checks"].tolist() == want, f"rank {r}: start-up checks {d['checks'].tolist()}"
+    assert len({int(d["digest"]) for d in R}) == 1, "the ranks' replicated states differ"
     for r, d in enumerate(R):   # every rank holds the whole tree and the merged exports
         assert np.array_equal(d["log"], o.iter_logs()), f"rank {r}: iteration logs differ"
         assert np.array_equal(d["p"], po), f"rank {r}: parents differ"

@@ -6,6 +6,8 @@
 #   tools/gpu_cycle.sh tests_k <out> <expr>        the -m gpu tests matching -k <expr>
 #   tools/gpu_cycle.sh ab <out> <reps> name=dir..  A/B of the driver's bench form (20 after 5)
 #                                                  and a 300-step line, runs interleaved
+#   tools/gpu_cycle.sh abenv <out> <reps> name=VAR=v..  the same A/B in this tree, each side with one
+#                                                  environment setting (e.g. off=SBMP_OVERLAP=0 on=SBMP_OVERLAP=1)
 #   tools/gpu_cycle.sh timeline <out> <dir> <it>.. k_step phase stamps at iterations <it> from the
 #                                                  stamped build in <dir> (tools/mk_variant.sh tl)
 #   tools/gpu_cycle.sh sq <out> [bench args]       one SQ counter pass (tools/pmc_summary.py)
@@ -46,6 +48,19 @@ ab)
                 k=${cfg%%:*}; w=${cfg#*:}; f="$R/$out/${name}_${k}_$rep.json"
                 (cd "$dir" && timeout -k 10 200 python3 bench.py --no-cpu-baseline --no-ttfs --steps "$k" --warmup "$w" \
                     > "$f" 2> "$f.err") || { echo "bench $name rc=$?"; tail -5 "$f.err"; exit 1; }
+                line "$f" "$name K=$k"
+            done
+        done
+    done ;;
+abenv)
+    reps=$1; shift
+    for rep in $(seq 1 "$reps"); do
+        for spec in "$@"; do
+            name=${spec%%=*}; kv=${spec#*=}
+            for cfg in 20:5 300:20; do
+                k=${cfg%%:*}; w=${cfg#*:}; f="$R/$out/${name}_${k}_$rep.json"
+                env "$kv" timeout -k 10 200 python3 bench.py --no-cpu-baseline --no-ttfs --steps "$k" --warmup "$w" \
+                    > "$f" 2> "$f.err" || { echo "bench $name rc=$?"; tail -5 "$f.err"; exit 1; }
                 line "$f" "$name K=$k"
             done
         done
