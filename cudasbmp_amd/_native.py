@@ -90,7 +90,7 @@ class InsertBatchArgs(ctypes.Structure):   # sbmp_insert_batch_args
 class PathInfo(ctypes.Structure):   # sbmp_path_info
     _fields_ = [(n, ctypes.c_int) for n in ("stepForm", "obstacleForm", "residentGroups", "neededGroups", "exchange",
                                             "nranks", "rank", "commRanks", "listMirror",
-                                            "fusedExchange", "overlap", "oneshotCheck", "mirrorCheck")]
+                                            "fusedExchange", "oneshotCheck", "mirrorCheck")]
 
 
 class KernelStat(ctypes.Structure):
@@ -104,7 +104,7 @@ EXPORTED_SYMBOLS = (
     "sbmp_kgmt_enqueue", "sbmp_kgmt_sync", "sbmp_kgmt_fold", "sbmp_kgmt_result", "sbmp_kgmt_stream", "sbmp_kgmt_copy_tree",
     "sbmp_kgmt_copy_unexplored", "sbmp_kgmt_copy_flags", "sbmp_kgmt_copy_regions", "sbmp_kgmt_num_slots",
     "sbmp_kgmt_copy_rng", "sbmp_kgmt_iter_log", "sbmp_kgmt_export_csv", "sbmp_kgmt_kernel_stats", "sbmp_kgmt_path_info",
-    "sbmp_kgmt_reset_kernel_stats", "sbmp_kgmt_set_profiling", "sbmp_kgmt_set_overlap", "sbmp_kgmt_state_hash", "sbmp_kgmt_kernel_samples", "sbmp_kgmt_enqueue_delay",
+    "sbmp_kgmt_reset_kernel_stats", "sbmp_kgmt_set_profiling", "sbmp_kgmt_state_hash", "sbmp_kgmt_kernel_samples", "sbmp_kgmt_enqueue_delay",
     "sbmp_read_obstacles_csv", "sbmp_device_upload_f32", "sbmp_device_free",
     "sbmp_device_count", "sbmp_comm_get_unique_id", "sbmp_kgmt_create_sharded", "sbmp_kgmt_create_local_group",
     "sbmp_kgmt_create_sharded_host", "sbmp_expand_batch", "sbmp_expand_batch_host", "sbmp_insert_batch",
@@ -170,7 +170,6 @@ def lib():
         "sbmp_kgmt_path_info": [vp, vp],
         "sbmp_kgmt_reset_kernel_stats": [vp],
         "sbmp_kgmt_set_profiling": [vp, i],
-        "sbmp_kgmt_set_overlap": [vp, i],
         "sbmp_kgmt_state_hash": [vp, P(ctypes.c_uint64)],
         "sbmp_kgmt_kernel_samples": [vp, ctypes.c_char_p, vp, i, P(i)],
         "sbmp_kgmt_enqueue_delay": [vp, ctypes.c_double],

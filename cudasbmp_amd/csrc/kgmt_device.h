@@ -58,7 +58,6 @@ struct PlannerStatus {
 // PlannerStatus::error: which bounded wait gave up.
 constexpr int kErrStepHandoff = 1;   // k_step: the planner workgroup's tagged scores/snapshot never arrived
 constexpr int kErrExchange = 2;      // k_oneshot: a peer rank's inbox flag never arrived
-constexpr int kErrStepOverlap = 3;   // overlapped k_step: the previous launch's workgroups never all arrived
 // Bounds of those waits, in ticks of the 100 MHz s_memrealtime clock.  The in-launch
 // hand-off waits for a workgroup of the same launch (1 s); the exchange waits for
 // other processes, whose kernels may start seconds apart (startup, code loading,
@@ -114,13 +113,6 @@ constexpr int kRecordF4 = 3;   // sharded record: state, ctrl (a, steer, dur, pa
 // buffer, then the compact layout's region starts and total.
 constexpr int kFxCounters = 9;   // fused exchange: 8 arrival shards + the top counter
 constexpr int kFxStride = 32;    // u32 words between counters (128 B)
-// Overlapped k_step: the arrival counters of the launches live in the
-// status allocation, behind PlannerStatus (k_step gets that pointer as a preloaded
-// argument): 8 shards (workgroup index mod 8) and the top counter, each on a 128-B line
-// of its own.  Monotonic over a plan (begin() zeroes them): launch t's workgroups add
-// one each to their shard, a shard's last arrival of launch t adds one to the top.
-constexpr int kDoneWordOff = 32;   // u32 words: 128 B past the status block's start
-constexpr int kStatusWords = kDoneWordOff + kFxCounters * kFxStride;
 struct OneshotCompact {
     int nR1, rowOff, rowWords, cntOff, owned, nBlocks, newOff, newWords;
     int cR, cB, cN, total;
@@ -310,34 +302,6 @@ __device__ __forceinline__ void store_wt(float* base, int i, float v) {
 }
 __device__ __forceinline__ void store_wt(uint32_t* base, int i, uint32_t v) {
     __builtin_amdgcn_raw_buffer_store_b32(v, wt_rsrc(base), SBMP_WT_OFF(i, 4), kCpolSc1);
-}
-
-// Loads of bytes that an earlier launch wrote while this one may already run (the
-// overlapped k_step), or that another workgroup of this launch wrote
-// through: sc1 loads bypass this CU's L1, which may still hold the line from before it
-// was rewritten (MI355X_MICROARCH.md, inter-workgroup visibility: the hand-off row
-// "sc1 stores, drained, one agent-scope add per workgroup, sc1 loads").  `base` must be
-// wave-uniform (the V# lives in SGPRs); `off` is a byte offset below 2^31.
-__device__ __forceinline__ sbmp_u32x4 ld_sc1_x4(const void* base, int off) {
-    return __builtin_amdgcn_raw_buffer_load_b128(wt_rsrc(base), off, 0, kCpolSc1);
-}
-__device__ __forceinline__ sbmp_u32x2 ld_sc1_x2(const void* base, int off) {
-    return __builtin_amdgcn_raw_buffer_load_b64(wt_rsrc(base), off, 0, kCpolSc1);
-}
-__device__ __forceinline__ uint32_t ld_sc1_x1(const void* base, int off) {
-    return __builtin_amdgcn_raw_buffer_load_b32(wt_rsrc(base), off, 0, kCpolSc1);
-}
-__device__ __forceinline__ float4 ld_sc1_f4(const void* base, int off) {
-    const sbmp_u32x4 v = ld_sc1_x4(base, off);
-    return make_float4(__uint_as_float(v[0]), __uint_as_float(v[1]), __uint_as_float(v[2]), __uint_as_float(v[3]));
-}
-__device__ __forceinline__ int4 ld_sc1_i4(const void* base, int off) {
-    const sbmp_u32x4 v = ld_sc1_x4(base, off);
-    return make_int4((int)v[0], (int)v[1], (int)v[2], (int)v[3]);
-}
-__device__ __forceinline__ unsigned long long ld_sc1_u64(const void* base, int off) {
-    const sbmp_u32x2 v = ld_sc1_x2(base, off);
-    return ((unsigned long long)v[1] << 32) | v[0];
 }
 
 // Slot i's XORWOW state for i < n, zeros with no memory access for i >= n: the

@@ -1183,32 +1183,13 @@ void launch_mirror_probe(const MirrorProbe& a, int phase, int pass, float* sink,
 // expand == 0 is the flush pass run before a read-back (no expansion; the same
 // values are rewritten by k_step(t) proper, so it is idempotent).
 // OR of word w over the kNewReps R2New replicas ([rep][nW] layout: one line per replica)
-// of ring slot `ring` (sc1 loads: the overlapped form reads them behind step_wait_prev)
-__device__ __forceinline__ uint32_t merge_new(const KgmtDev& d, int ring, int nW, int w) {
+__device__ __forceinline__ uint32_t merge_new(const SBMP_GAS uint32_t* p, int nW, int w) {
     uint32_t v = 0u;
 #pragma unroll
-    for (int r = 0; r < kNewReps; ++r) v |= ld_sc1_x1(d.stepR2New, (int)(((size_t)(ring * kNewReps + r) * nW + w) * 4));
+    for (int r = 0; r < kNewReps; ++r) v |= p[(size_t)r * nW + w];
     return v;
 }
 
-// ctrl[t-1] with sc1 loads (fields run .. scoreBuf: three 16-B loads of the 64-B line)
-__device__ __forceinline__ IterCtrl ld_ctrl(const IterCtrl* p) {
-    const sbmp_u32x4 a = ld_sc1_x4(p, 0), b = ld_sc1_x4(p, 16), c = ld_sc1_x4(p, 32);
-    IterCtrl r;
-    r.run = (int)a[0];
-    r.executed = (int)a[1];
-    r.treeSize = (int)a[2];
-    r.gLo = (int)a[3];
-    r.nG = (int)b[0];
-    r.k = (int)b[1];
-    r.nExp = (int)b[2];
-    r.S = (int)b[3];
-    r.H = (int)c[0];
-    r.A = (int)c[1];
-    r.scoreBuf = (int)c[2];
-    for (int i = 0; i < 5; ++i) r.pad[i] = 0;
-    return r;
-}
 // ctrl[t] written through (lane-uniform value, one thread stores)
 __device__ __forceinline__ void st_ctrl(IterCtrl* base, int t, const IterCtrl& c) {
     uint4* const q = reinterpret_cast<uint4*>(base + t);
@@ -1216,56 +1197,6 @@ __device__ __forceinline__ void st_ctrl(IterCtrl* base, int t, const IterCtrl& c
     store_wt(q, 1, make_uint4(c.nG, c.k, c.nExp, c.S));
     store_wt(q, 2, make_uint4(c.H, c.A, c.scoreBuf, c.pad[0]));
     store_wt(q, 3, make_uint4(c.pad[1], c.pad[2], c.pad[3], c.pad[4]));
-}
-
-// ---- overlapped k_step: consecutive launches on two alternating
-// streams, with no stream dependency between them; launch t's workgroups wait here for
-// every workgroup of launch t-1 instead of a kernel boundary.  The hand-off is the
-// guide's "sc1 stores, drained, one agent-scope add per workgroup, sc1 loads" row
-// (MI355X_MICROARCH.md, inter-workgroup visibility): everything k_step writes for a
-// later launch is stored sc1 (store_wt, atomics), every wave drains its stores before
-// its workgroup arrives, and every load of those bytes is an sc1 load.
-// The counters (kDoneWordOff, kgmt_device.h) sit behind the status block.
-__device__ __forceinline__ SBMP_GAS unsigned* done_counters(const PlannerStatus* st) {
-    return (SBMP_GAS unsigned*)(const_cast<PlannerStatus*>(st)) + kDoneWordOff;   // C cast: address space
-}
-// One lane polls the top counter (relaxed sc1 loads, s_sleep between) until the shards
-// of launch t-1 are all in (shards per launch: min(8, workgroups)); the other waves wait
-// at the barrier.  Bounded: a timeout sets status.error, which the host raises.
-__device__ __forceinline__ void step_wait_prev(const PlannerStatus* st, int t, int shards) {
-    if (threadIdx.x == 0 && t > 1) {
-        const SBMP_GAS unsigned* const top = done_counters(st) + 8 * kFxStride;
-        const unsigned want = (unsigned)(t - 1) * (unsigned)shards;
-        if ((int)(__hip_atomic_load(top, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - want) < 0) {
-            const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
-            for (;;) {
-                __builtin_amdgcn_s_sleep(2);
-                if ((int)(__hip_atomic_load(top, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - want) >= 0) break;
-                if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > kStepWaitTicks) {   // report, do not hang
-                    __hip_atomic_exchange(&G(const_cast<PlannerStatus*>(st))->error, kErrStepOverlap, __ATOMIC_RELAXED,
-                                          __HIP_MEMORY_SCOPE_AGENT);
-                    break;
-                }
-            }
-        }
-    }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // no instruction: keeps the loads below the poll
-    __syncthreads();
-}
-// Every wave's stores have completed, then lane 0 adds one to its shard (workgroup index
-// mod 8); the shard's last arrival of launch t (its count reaches t x its workgroups per
-// launch: arrivals of t+1 cannot start before all of t's) adds one to the top counter.
-__device__ __forceinline__ void step_arrive(const PlannerStatus* st, int t, int groups) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        SBMP_GAS unsigned* const c = done_counters(st);
-        const int s = (int)(blockIdx.x & 7);
-        const unsigned per = (unsigned)((groups - s + 7) >> 3);
-        const unsigned old = __hip_atomic_fetch_add(c + s * kFxStride, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (old + 1u == (unsigned)t * per)
-            __hip_atomic_fetch_add(c + 8 * kFxStride, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
 }
 
 __device__ __forceinline__ void step_unpack(int v, int* cnt, int* goal) {
@@ -1442,11 +1373,6 @@ __device__ __forceinline__ float4 list_load(const KgmtDev& d, const SBMP_GAS flo
     if (SH && !d.listPlain) return load_record_g(p);
     return *p;
 }
-// A single rank's list entry of row j: byte offset of (block lo, index i) in stepList
-// ([2][nBlocks * kBlock][kStepEntry] float4: < 2^31 B), read with sc1 loads.
-__device__ __forceinline__ int list_off(const KgmtDev& d, int pp, int lo, int i) {
-    return (int)((((size_t)pp * d.nBlocks + lo) * kBlock + i) * kStepEntry * 16);
-}
 
 // Plan scalars of iteration t from t-1's control block and the scan (KGMT.cu:118,
 // 139-188,249-259); every workgroup derives the same values.
@@ -1519,31 +1445,26 @@ __device__ __forceinline__ void step_planner(const KgmtDev& d, const ShardView& 
     if (tl) G(d.timelineFin)[0] = (long long)__builtin_amdgcn_s_memrealtime();
     // every input at entry
     // t-1's packed counts: blocks, or (sharded) rows of the exchange
-    // Everything k_step(t-1) (or earlier) wrote is read with sc1 loads (the overlapped
-    // form, step_wait_prev); the plan struct and the obstacles are constant.
-    const int4 pk = SH ? ld_sc1_i4(d.stepXr + d.xRowOff, tid * 16) : ld_sc1_i4(d.stepCnt, (pp * kMaxStepBlocks + tid * 4) * 4);
-    const IterCtrl pc = ld_ctrl(d.ctrl + (t - 1));
-    const int goalIdx = (int)ld_sc1_x1(d.status, 0);
-    const int* const tabPrev = d.R1 + (size_t)pp * 5 * d.nR1;
-    int r1 = (int)ld_sc1_x1(tabPrev, cell * 4), r1a = (int)ld_sc1_x1(tabPrev, (d.nR1 + cell) * 4),
-        r1v = (int)ld_sc1_x1(tabPrev, (2 * d.nR1 + cell) * 4), r1i = (int)ld_sc1_x1(tabPrev, (3 * d.nR1 + cell) * 4),
-        r1c = (int)ld_sc1_x1(tabPrev, (4 * d.nR1 + cell) * 4);
+    const int4 pk = SH ? reinterpret_cast<const SBMP_GAS int4*>(G(d.stepXr) + d.xRowOff)[tid]
+                       : *reinterpret_cast<const SBMP_GAS int4*>(G(d.stepCnt) + (size_t)pp * kMaxStepBlocks + tid * 4);
+    const IterCtrl pc = G(d.ctrl)[t - 1];
+    const int goalIdx = G(d.status)->goalIdx;
+    const SBMP_GAS int* tabPrev = G(d.R1) + (size_t)pp * 5 * d.nR1;
+    int r1 = tabPrev[cell], r1a = tabPrev[d.nR1 + cell], r1v = tabPrev[2 * d.nR1 + cell],
+        r1i = tabPrev[3 * d.nR1 + cell], r1c = tabPrev[4 * d.nR1 + cell];
     // sharded: the exchange's sum over ranks; else ring (t - 1) % 3
+    const SBMP_GAS unsigned long long* deltaPrev =
+        SH ? G(d.stepXr) : G(d.stepDelta) + (size_t)((t - 1) % 3) * kDeltaReps * d.nR1;
     unsigned long long dl = 0ull;   // replicas: carry-free sums
-    if constexpr (SH) {
 #pragma unroll
-        for (int r = 0; r < kDeltaReps; ++r) dl += G(d.stepXr)[(size_t)r * d.nR1 + cell];
-    } else {
-        const unsigned long long* const deltaPrev = d.stepDelta + (size_t)((t - 1) % 3) * kDeltaReps * d.nR1;
-#pragma unroll
-        for (int r = 0; r < kDeltaReps; ++r) dl += ld_sc1_u64(deltaPrev, (r * d.nR1 + cell) * 8);
-    }
-    const uint32_t* const availPrev = d.R2Avail + (size_t)pp * nW;
+    for (int r = 0; r < kDeltaReps; ++r) dl += deltaPrev[(size_t)r * d.nR1 + cell];
+    const SBMP_GAS uint32_t* availPrev = G(d.R2Avail) + (size_t)pp * nW;
+    const SBMP_GAS uint32_t* newPrev = G(d.stepR2New) + (size_t)((t - 1) % 3) * kNewReps * nW;
     uint32_t availW[kW], newW[kW];
 #pragma unroll
     for (int j = 0; j < kW; ++j) {
         const int w = min(tid + j * kBlock, nW - 1);
-        availW[j] = ld_sc1_x1(availPrev, w * 4);
+        availW[j] = availPrev[w];
         newW[j] = 0u;
     }
     // the R2New replicas: n <= 8 (two words per thread) with all 16 loads in flight;
@@ -1568,12 +1489,12 @@ __device__ __forceinline__ void step_planner(const KgmtDev& d, const ShardView& 
             }
         }
     } else if (nW <= 2 * kBlock) {
-        newW[0] = merge_new(d, (t - 1) % 3, nW, min(tid, nW - 1));
-        newW[1] = merge_new(d, (t - 1) % 3, nW, min(tid + kBlock, nW - 1));
+        newW[0] = merge_new(newPrev, nW, min(tid, nW - 1));
+        newW[1] = merge_new(newPrev, nW, min(tid + kBlock, nW - 1));
     } else {
 #pragma unroll
         for (int j = 0; j < kW; ++j)
-            if (j * kBlock < nW) newW[j] = merge_new(d, (t - 1) % 3, nW, min(tid + j * kBlock, nW - 1));
+            if (j * kBlock < nW) newW[j] = merge_new(newPrev, nW, min(tid + j * kBlock, nW - 1));
     }
     for (int i = tid; i < d.nR1; i += kBlock) sCovInc[i] = 0;
     int A, jGoal;
@@ -1588,8 +1509,8 @@ __device__ __forceinline__ void step_planner(const KgmtDev& d, const ShardView& 
     const StepPlan q = step_plan(d, t, expand, pc, goalIdx, A, jGoal);
     int* const tabCur = d.R1 + (size_t)cp * 5 * d.nR1;   // written through, like everything below
     if (!q.ranPrev) {   // t-1 did not run: the loop has ended; carry the tables forward
-        for (int i = tid; i < 5 * d.nR1; i += kBlock) store_wt(tabCur, i, (int)ld_sc1_x1(tabPrev, i * 4));
-        for (int i = tid; i < nW; i += kBlock) store_wt(d.R2Avail + (size_t)cp * nW, i, ld_sc1_x1(availPrev, i * 4));
+        for (int i = tid; i < 5 * d.nR1; i += kBlock) store_wt(tabCur, i, (int)tabPrev[i]);
+        for (int i = tid; i < nW; i += kBlock) store_wt(d.R2Avail + (size_t)cp * nW, i, (uint32_t)availPrev[i]);
         if (tid == 0) {
             IterCtrl c{};
             c.run = 0;
@@ -1732,34 +1653,15 @@ __device__ __forceinline__ void step_planner(const KgmtDev& d, const ShardView& 
             store_wt(d.treeCtrl + q.tsPrev, j, make_float4(u4.x, u4.y, u4.z, c));   // cost = parent's + duration (KGMT.cu:631-633)
             store_wt(d.treeParent + q.tsPrev, j, __float_as_int(u4.w));
         };
-        if constexpr (SH) {
-            for (int j0 = tid; j0 < n; j0 += 2 * kBlock) {   // two rows per thread per round, loads first
-                const int j1 = j0 + kBlock;
-                const SBMP_GAS float4* e0 = entry(j0);
-                const SBMP_GAS float4* e1 = entry(min(j1, n - 1));
-                const float4 s0 = list_load<SH>(d, e0), u0 = list_load<SH>(d, e0 + 1), s1 = list_load<SH>(d, e1),
-                             u1 = list_load<SH>(d, e1 + 1);
-                const float c0 = list_load<SH>(d, e0 + 2).x, c1 = list_load<SH>(d, e1 + 2).x;
-                put(j0, s0, u0, c0);
-                if (j1 < n) put(j1, s1, u1, c1);
-            }
-        } else {
-            auto off = [&](int j) {   // byte offset of row j's list entry
-                int lo = 0;
-                for (int step = kMaxStepBlocks / 2; step > 0; step >>= 1)
-                    if (lo + step < nS && sPfx[lo + step] <= j) lo += step;
-                return list_off(d, pp, lo, j - sPfx[lo]);
-            };
-            for (int j0 = tid; j0 < n; j0 += 2 * kBlock) {   // two rows per thread per round, loads first
-                const int j1 = j0 + kBlock;
-                const int o0 = off(j0), o1 = off(min(j1, n - 1));
-                const float4 s0 = ld_sc1_f4(d.stepList, o0), u0 = ld_sc1_f4(d.stepList, o0 + 16),
-                             s1 = ld_sc1_f4(d.stepList, o1), u1 = ld_sc1_f4(d.stepList, o1 + 16);
-                const float c0 = __uint_as_float(ld_sc1_x1(d.stepList, o0 + 32)),
-                            c1 = __uint_as_float(ld_sc1_x1(d.stepList, o1 + 32));
-                put(j0, s0, u0, c0);
-                if (j1 < n) put(j1, s1, u1, c1);
-            }
+        for (int j0 = tid; j0 < n; j0 += 2 * kBlock) {   // two rows per thread per round, loads first
+            const int j1 = j0 + kBlock;
+            const SBMP_GAS float4* e0 = entry(j0);
+            const SBMP_GAS float4* e1 = entry(min(j1, n - 1));
+            const float4 s0 = list_load<SH>(d, e0), u0 = list_load<SH>(d, e0 + 1), s1 = list_load<SH>(d, e1),
+                         u1 = list_load<SH>(d, e1 + 1);
+            const float c0 = list_load<SH>(d, e0 + 2).x, c1 = list_load<SH>(d, e1 + 2).x;
+            put(j0, s0, u0, c0);
+            if (j1 < n) put(j1, s1, u1, c1);
         }
     }
 }
@@ -1792,14 +1694,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) voi
     const IterCtrl* __restrict__ ctrlPrev, const uint4* __restrict__ rngAArg, const uint2* __restrict__ rngBArg,
     const unsigned long long* __restrict__ gnewArg, const PlannerStatus* __restrict__ statusArg, long long* tlBase,
     int shRows, const int* __restrict__ shBw) {
-    // tx = t | overlapped << 30 | expand << 31 and shRR = rank | ranks << 8 | arrival
-    // shards << 16 share the preloaded argument dwords with the prologue's first pointers
-    // (a sharded slot index needs the rank before its first load)
-    const int t = tx & 0x3fffffff, expand = (int)((unsigned)tx >> 31);
-    const bool ovl = !SH && ((tx >> 30) & 1);   // overlapped launches (single rank)
+    // tx = t | expand << 31 and shRR = rank | ranks << 8 share the preloaded argument
+    // dwords with the prologue's first pointers (a sharded slot index needs the rank
+    // before its first load)
+    const int t = tx & 0x7fffffff, expand = (int)((unsigned)tx >> 31);
     const KgmtDev& d = *dp;
-    const ShardView sv{SH ? ((shRR >> 8) & 0xff) : 1, SH ? (shRR & 0xff) : 0, SH ? shRows : 0, G(shBw)};
-    if (ovl) step_wait_prev(statusArg, t, shRR >> 16);   // launch t-1 has ended, in software
+    const ShardView sv{SH ? (shRR >> 8) : 1, SH ? (shRR & 0xff) : 0, SH ? shRows : 0, G(shBw)};
     extern __shared__ float4 sDyn[];   // [LDS obstacles][prefix: nBlocks + 1 ints][R2New bits: nR2 / 32]
     __shared__ int sR1P[kMaxR1];
     __shared__ StepPlan sPlan;
@@ -1815,7 +1715,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) voi
     uint32_t* const sNew = reinterpret_cast<uint32_t*>(sPfx + (SH ? sv.nRows : d.nBlocks) + 1);
     if (blockIdx.x == 0) {
         step_planner<SH>(d, sv, t, expand, sPfx, sRed, sCovInc, sPart);
-        if (ovl) step_arrive(statusArg, t, 1 + d.nBlocks);
         if constexpr (SH) {
             if (expand && d.fusedX) step_planner_arrive(d, t);
         }
@@ -1850,21 +1749,23 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) voi
     // The first loads' pointers are preloaded arguments; the plan's scalars and the
     // next pointers in one batch of scalar loads from the struct (one round trip, in
     // flight with the vector loads below)
+    const SBMP_GAS IterCtrl* const ctrlP = G(ctrlPrev);
+    const SBMP_GAS PlannerStatus* const statusP = G(statusArg);
+    const SBMP_GAS uint4* const rngAP = G(rngAArg);
+    const SBMP_GAS uint2* const rngBP = G(rngBArg);
+    const SBMP_GAS unsigned long long* const gnewP = G(gnewArg);
     SBMP_STAMP(0);
 
     // ---- loads that depend on nothing else (the control block as a plain load: a
     // waiting scalar load would serialise behind the scan)
-    // (sc1 loads of everything an earlier k_step wrote: the overlapped form, step_wait_prev)
-    const int4 pk = ld_sc1_i4(cnt4, tid * 16);
-    const IterCtrl pc = ld_ctrl(ctrlPrev);
+    const int4 pk = G(cnt4)[tid];
+    const IterCtrl pc = *ctrlP;
     int rowW[SH ? kMaxRanks : 1];   // sharded: the block words of this workgroup's row (its inserts)
     if constexpr (SH) row_words(sv, b, rowW);
-    const int goalIdx = (int)ld_sc1_x1(statusArg, 0);
-    const sbmp_u32x4 ra4 = ld_sc1_x4(rngAArg, slot * 16);
-    const sbmp_u32x2 rb2 = ld_sc1_x2(rngBArg, slot * 8);
-    const uint4 ra = make_uint4(ra4[0], ra4[1], ra4[2], ra4[3]);
-    const uint2 rb = make_uint2(rb2[0], rb2[1]);
-    const unsigned long long oldWord = (lane == 0) ? ld_sc1_u64(gnewArg, (slot >> 6) * 8) : 0ull;
+    const int goalIdx = statusP->goalIdx;
+    const uint4 ra = rngAP[slot];
+    const uint2 rb = rngBP[slot];
+    const unsigned long long oldWord = (lane == 0) ? gnewP[slot >> 6] : 0ull;
     asm volatile("" ::"s"(d.M), "s"(d.nBlocks), "s"(d.numIterations), "s"(d.numDisc), "s"(d.nR1), "s"(d.nR2),
                  "s"(d.cap), "s"(d.fixGNewClear), "s"(d.batchRule), "s"(d.rcpNumDisc), "s"(d.treeState),
                  "s"(d.treeCtrl), "s"(d.stepList));
@@ -1954,10 +1855,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) voi
             const int j = j0 + tid;
             const int dst = q.tsPrev + j;
             if (j < q.nIns && dst < d.M) {   // D13: the reference writes past M here
-                const int o = list_off(d, pp, lo, tid);
-                const float4 s4 = ld_sc1_f4(d.stepList, o);
-                const float4 u4 = ld_sc1_f4(d.stepList, o + 16);
-                const float4 m4 = ld_sc1_f4(d.stepList, o + 32);
+                const SBMP_GAS float4* e = list_entry<SH>(d, pp, lo, tid);
+                const float4 s4 = list_load<SH>(d, e);
+                const float4 u4 = list_load<SH>(d, e + 1);
+                const float4 m4 = list_load<SH>(d, e + 2);
                 // written through (fewer dirty lines at the boundary); the V# based at row tsPrev keeps
                 // the byte offset j * 16 far below 2^31 whatever M is
                 store_wt(d.treeState + q.tsPrev, j, s4);
@@ -2008,9 +1909,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) voi
     }
     g = act ? g : 0;
     const int parent = act ? q.gLo + g : 0;
-    const SBMP_GAS float4* src = G(d.treeState) + parent;   // (sharded) the parent's state, and its cost
+    const SBMP_GAS float4* src = G(d.treeState) + parent;   // the parent's state, and its cost
     const SBMP_GAS float* srcCost = &G(d.treeCtrl)[parent].w;
-    int lOff = 0;   // single rank: byte offset of the parent's list entry (fromList)
     // A parent inserted by t-1 is read from its block's compacted list: block lo with
     // sPfx[lo] <= j < sPfx[lo + 1].  j grows with the lane; when a wave's parents are
     // at most two consecutive list positions jA, jB (k >= 32 children per parent) both
@@ -2054,29 +1954,21 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) voi
                 row_words(sv, lo, w);
                 row_locate(sv, w, lo, j - sPfx[lo], &blk, &idx);
                 src = list_entry<SH>(d, pp, blk, idx);
-                srcCost = reinterpret_cast<const SBMP_GAS float*>(src + 2);
             } else {
-                lOff = list_off(d, pp, lo, j - sPfx[lo]);
+                src = list_entry<SH>(d, pp, lo, j - sPfx[lo]);
             }
+            srcCost = reinterpret_cast<const SBMP_GAS float*>(src + 2);
         }
     }
     // Parent and obstacles are issued back to back and waited for together.
     float4 p;
     float parentCost;
-    if constexpr (SH) {
-        if (fromList && !d.listPlain) {   // the owner's list over the mapping: system-scope loads
-            p = load_record_g(src);
-            parentCost = load_record_g(src + 2).x;
-        } else {
-            p = *src;
-            parentCost = *srcCost;
-        }
-    } else if (fromList) {   // sc1 loads (a single rank's rows and lists may be an overlapped launch's)
-        p = ld_sc1_f4(d.stepList, lOff);
-        parentCost = __uint_as_float(ld_sc1_x1(d.stepList, lOff + 32));
-    } else {   // rows [gLo, gLo + nExp): offsets g * 16 from row gLo (inactive lanes: row gLo)
-        p = ld_sc1_f4(d.treeState + q.gLo, g * 16);
-        parentCost = __uint_as_float(ld_sc1_x1(d.treeCtrl + q.gLo, g * 16 + 12));
+    if (SH && fromList && !d.listPlain) {   // the owner's list over the mapping: system-scope loads
+        p = load_record_g(src);
+        parentCost = load_record_g(src + 2).x;
+    } else {
+        p = *src;
+        parentCost = *srcCost;
     }
     float4 ro[kRegObs > 0 ? kRegObs : 1];
 #pragma unroll
@@ -2211,10 +2103,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) voi
     const bool flagged = (wordAll >> lane) & 1ull;
     if ((wordAll & ~__ballot(act)) != 0ull) {   // rare; keeps the wait below off the common path
         if (flagged && !act) {   // a stale flag on a slot past S: the child last written there
-            cs = ld_sc1_f4(d.uState, slot * 16);
-            cc = ld_sc1_f4(d.uCtrl, slot * 16);
-            cost = __hip_atomic_load(&G(d.treeCtrl)[__float_as_int(cc.w)].w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) +
-                   cc.z;
+            cs = G(d.uState)[slot];
+            cc = G(d.uCtrl)[slot];
+            cost = G(d.treeCtrl)[__float_as_int(cc.w)].w + cc.z;
         }
     }
     bool inGoal = false;
@@ -2325,7 +2216,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) voi
     };
     body();
     fx_exit();
-    if (ovl) step_arrive(statusArg, t, 1 + d.nBlocks);
 #undef SBMP_STAMP
 }
 
@@ -2540,7 +2430,7 @@ void launch_expand(const KgmtDev& d, int t, int agent, int blocks, int variant, 
 
 template <int AGENT, bool SH>
 static void launch_step_form(const KgmtDev& d, int t, int expand, int variant, hipStream_t s,
-                             const KernelTiming& tm, int overlap) {
+                             const KernelTiming& tm) {
     // dynamic LDS: [LDS obstacles][block prefix: nBlocks + 1 ints][R2New bits: nR2 / 32 words]
     const size_t nS = SH ? d.nBlocks / d.nranks : d.nBlocks;   // scan entries: blocks, or rows
     const size_t pfx = sizeof(int) * (nS + 1) + sizeof(uint32_t) * (size_t)(d.nR2 / 32);
@@ -2551,13 +2441,9 @@ static void launch_step_form(const KgmtDev& d, int t, int expand, int variant, h
     long long* const tlBase = (d.timeline && t == d.timelineIter && expand) ? d.timeline : nullptr;
     const int4* const cnt4 = SH ? reinterpret_cast<const int4*>(d.stepXr + d.xRowOff)
                                 : reinterpret_cast<const int4*>(d.stepCnt + (size_t)((t - 1) & 1) * kMaxStepBlocks);
-    // overlapped launches (single rank, expanding passes only): the arrival shards per launch
-    const bool ovl = !SH && overlap && expand;
-    const int shards = std::min(8, 1 + blocks);
-#define SBMP_STEP_ARGS                                                                                          \
-    d.devSelf, (int)((unsigned)t | ((unsigned)ovl << 30) | ((unsigned)(expand != 0) << 31)),                     \
-        SH ? (d.rank | (d.nranks << 8)) : ((1 << 8) | (shards << 16)), cnt4, d.ctrl + (t - 1), d.rngA, d.rngB,     \
-        d.gnewOut, d.status, tlBase, SH ? d.nBlocks / d.nranks : d.nBlocks,                                      \
+#define SBMP_STEP_ARGS                                                                                        \
+    d.devSelf, (int)((unsigned)t | ((unsigned)(expand != 0) << 31)), SH ? (d.rank | (d.nranks << 8)) : (1 << 8),  \
+        cnt4, d.ctrl + (t - 1), d.rngA, d.rngB, d.gnewOut, d.status, tlBase, SH ? d.nBlocks / d.nranks : d.nBlocks, \
         SH ? reinterpret_cast<const int*>(d.stepXr + d.xCntOff) : nullptr
     if (d.gridStart) {
         launch(k_step<AGENT, kObsGrid, SH>, grid, block, pfx + gridLds, s, tm, SBMP_STEP_ARGS);
@@ -2638,15 +2524,15 @@ int step_resident_groups(const KgmtDev& d, int agent, int variant, StepResidency
 
 template <int AGENT>
 static void launch_step_agent(const KgmtDev& d, int t, int expand, int variant, hipStream_t s,
-                              const KernelTiming& tm, int overlap) {
-    if (d.sharded) launch_step_form<AGENT, true>(d, t, expand, variant, s, tm, overlap);
-    else launch_step_form<AGENT, false>(d, t, expand, variant, s, tm, overlap);
+                              const KernelTiming& tm) {
+    if (d.sharded) launch_step_form<AGENT, true>(d, t, expand, variant, s, tm);
+    else launch_step_form<AGENT, false>(d, t, expand, variant, s, tm);
 }
 
 void launch_step(const KgmtDev& d, int t, int expand, int agent, int variant, hipStream_t s,
-                 const KernelTiming& tm, int overlap) {
-    if (agent == 0) launch_step_agent<0>(d, t, expand, variant, s, tm, overlap);
-    else launch_step_agent<1>(d, t, expand, variant, s, tm, overlap);
+                 const KernelTiming& tm) {
+    if (agent == 0) launch_step_agent<0>(d, t, expand, variant, s, tm);
+    else launch_step_agent<1>(d, t, expand, variant, s, tm);
 }
 
 void launch_fold_r2(const KgmtDev& d, int tFirst, int tLast, hipStream_t s, const KernelTiming& tm) {

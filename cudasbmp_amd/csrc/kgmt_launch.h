@@ -23,11 +23,8 @@ void launch_expand(const KgmtDev& d, int t, int agent, int blocks, int variant, 
                    const KernelTiming& tm = KernelTiming());
 // k_fold_r2: add the key log of iterations [tFirst, tLast] (at most kFoldEvery) to R2Valid / R2Invalid.
 // k_step(t): one launch per iteration on a single rank; expand == 0: flush pass.
-// overlap (single rank, expanding passes): the launch waits in-kernel for every workgroup
-// of k_step(t-1), which may still run on another stream, and reports its own arrivals
-// (DESIGN.md §5.6); the counters are zeroed at begin().
 void launch_step(const KgmtDev& d, int t, int expand, int agent, int variant, hipStream_t s,
-                 const KernelTiming& tm = KernelTiming(), int overlap = 0);
+                 const KernelTiming& tm = KernelTiming());
 // Workgroups of the k_step form launch_step would pick for d that the device holds at
 // once (occupancy per CU x CUs); k_step needs all of its 1 + blocks resident, since
 // its expanders wait for workgroup 0.  0 if the query fails.

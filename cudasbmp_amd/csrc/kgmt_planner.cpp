@@ -87,8 +87,6 @@ static float markstein_rcp(float b) {
         throw Error(SBMP_ERR_COMM, "k_oneshot: a peer rank's exchange flag did not arrive within 20 s");
     if (e == kErrStepHandoff)
         throw Error(SBMP_ERR_HIP, "k_step: the planner workgroup's hand-off did not arrive within 1 s");
-    if (e == kErrStepOverlap)
-        throw Error(SBMP_ERR_HIP, "overlapped k_step: the previous launch's workgroups did not all arrive within 1 s");
     throw Error(SBMP_ERR_HIP, "in-kernel wait failed (status " + std::to_string(e) + ")");
 }
 
@@ -120,12 +118,6 @@ KgmtPlanner::KgmtPlanner(const sbmp_kgmt_params& p, int nranks, int rank, Exchan
     } else {
         SBMP_HIP(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
     }
-    if (!shared && nranks == 1 && !ex) {   // a single rank: the overlapped k_step's second stream (§5.6)
-        SBMP_HIP(hipStreamCreateWithFlags(&stream2_, hipStreamNonBlocking));
-        SBMP_HIP(hipEventCreateWithFlags(&evFork_, hipEventDisableTiming));
-        SBMP_HIP(hipEventCreateWithFlags(&evJoin_, hipEventDisableTiming));
-    }
-    if (const char* v = getenv("SBMP_OVERLAP")) overlapReq_ = atoi(v) ? 1 : 0;
     // Obstacle-list form of k_expand (diagnostics / A-B): 0 auto, 1 LDS, 2 LDS x4,
     // 3 registers, 4 grid index at any count, 5 global list without the grid.
     if (const char* v = getenv("SBMP_EXPAND_VARIANT")) expandVariant_ = std::min(5, std::max(0, atoi(v)));
@@ -292,10 +284,7 @@ KgmtPlanner::KgmtPlanner(const sbmp_kgmt_params& p, int nranks, int rank, Exchan
     d.logSlots = expandBlocks_ * kBlock;
     d.r2log = (d.nR2 <= kLogMaxR2) ? alloc<uint16_t>((size_t)kFoldEvery * d.logSlots) : nullptr;
     d.ctrl = alloc<IterCtrl>(p.numIterations + 2);
-    // the status block, then the overlapped k_step's arrival counters (kDoneWordOff)
-    static_assert(sizeof(PlannerStatus) <= kDoneWordOff * sizeof(unsigned), "counters behind the status block");
-    d.status = reinterpret_cast<PlannerStatus*>(alloc<unsigned>(kStatusWords));
-    SBMP_HIP(hipMemset(d.status, 0, sizeof(unsigned) * kStatusWords));
+    d.status = alloc<PlannerStatus>(1);
     SBMP_HIP(hipHostMalloc(reinterpret_cast<void**>(&poll_), sizeof(PollBuf), hipHostMallocDefault));
     d.timeline = nullptr;
     d.timelineFin = nullptr;
@@ -497,12 +486,8 @@ bool KgmtPlanner::mirror_self_test() {
 KgmtPlanner::~KgmtPlanner() {
     if (stream_) {
         (void)hipSetDevice(p_.device);
-        if (stream2_) (void)hipStreamSynchronize(stream2_);
         (void)hipStreamSynchronize(stream_);
     }
-    if (stream2_) (void)hipStreamDestroy(stream2_);
-    if (evFork_) (void)hipEventDestroy(evFork_);
-    if (evJoin_) (void)hipEventDestroy(evJoin_);
     for (auto& q : pending_) {
         (void)hipEventDestroy(q.a);
         (void)hipEventDestroy(q.b);
@@ -526,7 +511,6 @@ void KgmtPlanner::begin(const float* initial, const float* goal, const float* d_
         if (!std::isfinite(initial[i]))
             throw Error(SBMP_ERR_INVALID_ARGUMENT, "initial state (x, y, theta, v) must be finite");
     SBMP_HIP(hipSetDevice(p_.device));
-    join_streams();   // a previous plan's launches on the second stream come first
     KgmtDev& d = d_;
     hipStream_t s = stream_;
     // Constructor state (KGMT.cu:16-72): zero-filled vectors, parents -1, R1Score 1.0.
@@ -554,9 +538,6 @@ void KgmtPlanner::begin(const float* initial, const float* goal, const float* d_
     SBMP_HIP(hipMemsetAsync(d.R2Invalid, 0, sizeof(int) * d.nR2, s));
     launch_fill_f32(d.R1Score, 1.0f, 2 * d.nR1, s);
     SBMP_HIP(hipMemsetAsync(d.ctrl, 0, sizeof(IterCtrl) * (p_.numIterations + 2), s));
-    // the overlapped k_step's arrival counters count the launches of this plan
-    SBMP_HIP(hipMemsetAsync(reinterpret_cast<unsigned*>(d.status) + kDoneWordOff, 0,
-                            sizeof(unsigned) * (kStatusWords - kDoneWordOff), s));
 
     // Obstacles: a private float4 copy of the caller's device array (KGMT.cu:80 takes
     // d_obstacles by pointer; copying keeps the row layout 16-B aligned).
@@ -602,9 +583,6 @@ void KgmtPlanner::begin(const float* initial, const float* goal, const float* d_
     t_next_ = 1;
     lastFolded_ = 0;
     begun_ = true;
-    // overlapped launches: one rank in the k_step form, when asked (SBMP_OVERLAP=1 / sbmp_kgmt_set_overlap)
-    overlap_ = stream2_ && d.stepMode && !d.sharded && overlapReq_ != 0;
-    ovlRun_ = ovlNextAlt_ = ovlAltUsed_ = false;
     wallMs_ = 0.0;
     SBMP_HIP(hipStreamSynchronize(s));
     if (ex_) ex_->barrier(s);   // every rank set up before the first (time-bounded) exchange
@@ -672,7 +650,6 @@ void KgmtPlanner::path_info(sbmp_path_info* out) {
     out->commRanks = ex_ ? ex_->comm_ranks() : 0;
     out->listMirror = d.stepMirror ? 1 : 0;
     out->fusedExchange = d.fusedX ? 1 : 0;
-    out->overlap = overlap_ ? 1 : 0;
     out->oneshotCheck = oneshotCheck_;
     out->mirrorCheck = mirrorCheck_;
 }
@@ -752,40 +729,8 @@ void KgmtPlanner::stage_pack(int t) {
 
 void KgmtPlanner::stage_step(int t) {
     upload_dev();
-    launch_step(d_, t, 1, p_.agent, expandVariant_, step_stream(), timing(K_STEP), overlap_ ? 1 : 0);
+    launch_step(d_, t, 1, p_.agent, expandVariant_, stream_, timing(K_STEP));
     flushed_ = false;
-}
-
-// The stream of the next k_step launch.  Overlapped: the first launch after a join goes on
-// stream_, and stream2_ is forked from the point just before it, so that stream2_'s next
-// launch waits for everything before that launch and for nothing after it; from then on
-// the launches alternate.  A launch on one stream thus follows the launch two iterations
-// back (its stream predecessor) and whatever preceded the last join; it waits for the
-// launch just before it inside the kernel (step_wait_prev).
-hipStream_t KgmtPlanner::step_stream() {
-    if (!overlap_) return stream_;
-    if (!ovlRun_) {
-        SBMP_HIP(hipEventRecord(evFork_, stream_));
-        SBMP_HIP(hipStreamWaitEvent(stream2_, evFork_, 0));
-        ovlRun_ = true;
-        ovlNextAlt_ = true;
-        return stream_;
-    }
-    const bool alt = ovlNextAlt_;
-    ovlNextAlt_ = !ovlNextAlt_;
-    if (alt) ovlAltUsed_ = true;
-    return alt ? stream2_ : stream_;
-}
-
-// stream_ waits for what was enqueued on stream2_; anything other than an overlapped
-// k_step launch is enqueued on stream_ after this.
-void KgmtPlanner::join_streams() {
-    if (!ovlRun_) return;
-    if (ovlAltUsed_) {
-        SBMP_HIP(hipEventRecord(evJoin_, stream2_));
-        SBMP_HIP(hipStreamWaitEvent(stream_, evJoin_, 0));
-    }
-    ovlRun_ = ovlNextAlt_ = ovlAltUsed_ = false;
 }
 
 void KgmtPlanner::stage_exchange(int t) {
@@ -822,7 +767,6 @@ void KgmtPlanner::stage_exchange(int t) {
 
 // k_step mode: complete the last enqueued iteration (insert it, plan t_next) before a read-back
 void KgmtPlanner::flush() {
-    join_streams();
     if (d_.stepMode && begun_ && !flushed_) {
         upload_dev();
         launch_step(d_, t_next_, 0, p_.agent, expandVariant_, stream_, KernelTiming());
@@ -843,7 +787,6 @@ void KgmtPlanner::stage_fold(int t) {
 // Bring R2Valid / R2Invalid up to iteration tLast (k_fold_r2 over the key log).
 void KgmtPlanner::fold_to(int tLast) {
     if (tLast <= lastFolded_) return;
-    join_streams();
     if (d_.r2log) launch_fold_r2(d_, lastFolded_ + 1, tLast, stream_, timing(K_FOLD));
     lastFolded_ = tLast;
 }
@@ -853,7 +796,6 @@ void KgmtPlanner::fold_to(int tLast) {
 void KgmtPlanner::upload_dev() {
     if (!dDev_) throw Error(SBMP_ERR_STATE, "k_step: the plan struct has no device copy");
     if (uploaded_ && std::memcmp(&d_, dStage_, sizeof(KgmtDev)) == 0) return;
-    join_streams();   // the copy goes on stream_, behind every launch that reads the old one
     if (uploaded_) SBMP_HIP(hipStreamSynchronize(stream_));   // the previous copy has been read
     std::memcpy(dStage_, &d_, sizeof(KgmtDev));
     SBMP_HIP(hipMemcpyAsync(dDev_, dStage_, sizeof(KgmtDev), hipMemcpyHostToDevice, stream_));
@@ -861,7 +803,7 @@ void KgmtPlanner::upload_dev() {
 }
 
 void KgmtPlanner::sync() {
-    flush();   // joins the second stream first
+    flush();
     SBMP_HIP(hipStreamSynchronize(stream_));
     wallMs_ = now_ms() - t0_;
     if (d_.timeline && !timelineDumped_ && t_next_ > d_.timelineIter) {

@@ -86,7 +86,6 @@ public:
     virtual void reset_kernel_stats() = 0;
     virtual void set_profiling(bool on) = 0;
     virtual void enqueue_delay(double us) = 0;
-    virtual void set_overlap(int) {}   // overlapped k_step launches from the next begin() (single rank)
     virtual std::vector<float> kernel_samples(const std::string& name) = 0;
 
 protected:
@@ -139,11 +138,7 @@ public:
     void path_info(sbmp_path_info* out) override;
     void reset_kernel_stats() override;
     void set_profiling(bool on) override { p_.profileKernels = on ? 1 : 0; }
-    void enqueue_delay(double us) override {
-        join_streams();
-        launch_delay(us, stream_);
-    }
-    void set_overlap(int on) override { overlapReq_ = on ? 1 : 0; }   // from the next begin()
+    void enqueue_delay(double us) override { launch_delay(us, stream_); }
     std::vector<float> kernel_samples(const std::string& name) override;
 
     // ---- stages of one iteration (enqueue() composes them; a LocalShardGroup
@@ -184,20 +179,6 @@ private:
     void upload_dev();
     hipStream_t stream_ = nullptr;
     bool ownStream_ = true;
-    // Overlapped k_step launches (single rank): consecutive iterations
-    // alternate between stream_ and stream2_ with no stream dependency; k_step(t) waits
-    // in-kernel for k_step(t-1).  Anything else enqueued (fold, flush, copies) first joins
-    // stream2_ into stream_ (join_streams); the first launch after a join goes on stream_
-    // and forks stream2_ from the point just before it.
-    hipStream_t stream2_ = nullptr;
-    hipEvent_t evFork_ = nullptr, evJoin_ = nullptr;
-    int overlapReq_ = 0;       // sbmp_kgmt_set_overlap / SBMP_OVERLAP=1 (off by default: §5.6 measures it slower)
-    bool overlap_ = false;     // this plan launches overlapped (decided at begin())
-    bool ovlRun_ = false;      // launches since the last join alternate
-    bool ovlNextAlt_ = false;  // the next launch goes on stream2_
-    bool ovlAltUsed_ = false;  // stream2_ holds launches stream_ has not joined
-    void join_streams();
-    hipStream_t step_stream();
     Exchange* ex_ = nullptr;
     int t_next_ = 1;
     bool begun_ = false;

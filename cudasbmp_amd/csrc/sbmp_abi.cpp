@@ -417,12 +417,6 @@ sbmp_status sbmp_kgmt_state_hash(sbmp_kgmt* h, uint64_t* out) {
     });
 }
 
-sbmp_status sbmp_kgmt_set_overlap(sbmp_kgmt* h, int enabled) {
-    return guarded([&] {
-        PLANNER(h);
-        P.set_overlap(enabled != 0);
-    });
-}
 
 // readObstaclesFromCSV (reference src/helper/helper.cu:11-34): values separated
 // by whitespace or single commas, read line by line with operator>>.

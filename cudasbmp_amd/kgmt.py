@@ -334,7 +334,6 @@ class KGMT:
                 "exchange": self.EXCHANGES[pi.exchange] if 0 <= pi.exchange < 3 else pi.exchange,
                 "nranks": pi.nranks, "rank": pi.rank, "rccl_nranks": pi.commRanks,
                 "list_mirror": bool(pi.listMirror), "fused_exchange": bool(pi.fusedExchange),
-                "overlap": bool(pi.overlap),
                 "oneshot_check": {0: "not run", 1: "passed", -1: "failed"}.get(pi.oneshotCheck, pi.oneshotCheck),
                 "mirror_check": {0: "not run", 1: "passed", -1: "failed"}.get(pi.mirrorCheck, pi.mirrorCheck)}
 
@@ -360,6 +359,3 @@ class KGMT:
         nat.call("sbmp_kgmt_state_hash", self._h, ctypes.byref(h))
         return int(h.value)
 
-    def set_overlap(self, enabled: bool) -> None:
-        """Overlapped k_step launches (one rank; on by default) from the next begin() / plan()."""
-        nat.call("sbmp_kgmt_set_overlap", self._h, int(bool(enabled)))

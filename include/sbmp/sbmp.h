@@ -116,8 +116,6 @@ typedef struct sbmp_path_info {
                                  rank's mirror, and k_step reads its parents from local HBM */
     int fusedExchange;        /* 1: the last expanding workgroup of k_step runs the one-shot exchange
                                  (no k_oneshot launch) */
-    int overlap;              /* 1: consecutive k_step launches alternate between two streams and each
-                                 waits in-kernel for the previous one (one rank) */
     int oneshotCheck;         /* start-up check of the one-shot exchange: 0 not run, 1 passed,
                                  -1 failed on some rank (every rank then uses the all-reduce) */
     int mirrorCheck;          /* start-up check of the list mirror (stores into peers' mirrors
@@ -225,11 +223,6 @@ sbmp_status sbmp_kgmt_set_profiling(sbmp_kgmt* h, int enabled);
  * blocks (no reference counterpart).  Every rank of a sharded run holds the same replica,
  * so every rank's digest must be equal: bench.py --gpus N checks it (replicas_agree). */
 sbmp_status sbmp_kgmt_state_hash(sbmp_kgmt* h, uint64_t* out);
-/* Overlapped k_step launches (one rank; off by default, DESIGN.md §5.6 measures them
- * slower on MI355X; no reference counterpart: the reference's loop, KGMT.cu:118-292,
- * blocks on the device every iteration): 1 turns them on, 0 off, from the next
- * begin()/plan().  Results are identical either way. */
-sbmp_status sbmp_kgmt_set_overlap(sbmp_kgmt* h, int enabled);
 /* Queue a device-side delay (bounded spin on the GPU clock) so that the
  * launches enqueued after it execute back to back, as in an un-instrumented run. */
 sbmp_status sbmp_kgmt_enqueue_delay(sbmp_kgmt* h, double microseconds);

@@ -32,14 +32,12 @@ pytestmark = pytest.mark.gpu
 BENCH_SEED = 20240807
 
 
-def _run(kw, seed, obs, P=0, threads=16, overlap=None):
+def _run(kw, seed, obs, P=0, threads=16):
     from cudasbmp_amd import KGMT, DeviceBuffer
     cfg = dict(DEMO)
     extra = {k: kw[k] for k in ("samplesPerIteration", "agent", "fixGNewClear", "batchRule") if k in kw}
     cfg.update({k: v for k, v in kw.items() if k not in extra})
     g = KGMT(**cfg, **extra, _local_group=P)
-    if overlap is not None:
-        g.set_overlap(overlap)
     r = g.plan(DEMO_INITIAL, DEMO_GOAL, DeviceBuffer(obs), len(obs), seed=seed)
     o = _oracle(cfg, extra, threads=threads)
     o.plan(DEMO_INITIAL, DEMO_GOAL, obs, seed)
@@ -75,14 +73,10 @@ def test_c1_as_configured_bit_exact(oracle_lib):
     assert_same_state(g, o, label="c1 as configured")
 
 
-@pytest.mark.parametrize("overlap", [True, False], ids=["overlapped", "serial"])
-def test_c3_bench_mode_bit_exact(obstacles, oracle_lib, overlap):
-    """Both launch forms of one rank: overlapped k_step launches on two streams, each
-    waiting in-kernel for the previous one (the default), and one
-    stream with a kernel boundary per iteration."""
-    g, o, r = _run(_bench_kw(262144, 72), BENCH_SEED, obstacles, overlap=overlap)
+def test_c3_bench_mode_bit_exact(obstacles, oracle_lib):
+    g, o, r = _run(_bench_kw(262144, 72), BENCH_SEED, obstacles)
     info = g.path_info()
-    assert info["form"] == "k_step" and info["overlap"] == overlap, info
+    assert info["form"] == "k_step", info
     log = g.iter_log()
     assert r.iterations == 72 and log[5:, 5].min() > 250000
     assert (log[20:, 6] <= 4096).all(), "steady state: the planner workgroup inserts"
