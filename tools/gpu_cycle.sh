@@ -16,6 +16,8 @@
 #   tools/gpu_cycle.sh bench <out> <name> [args]   one bench line into <out>/<name>.json
 #   tools/gpu_cycle.sh shard <out>                 tools/shard_cost.py 1 2 8 and two ranks on one GPU
 #   tools/gpu_cycle.sh attrib <out> <wl> <n> <it>  per-launch traffic fitted per child (tools/write_attrib.py)
+#   tools/gpu_cycle.sh wlpmc <out> <wl> <n> <N> <first> <last>  SQ / FETCH / WRITE of k_step summed over
+#                                                  iterations first..last of one seeded run (tools/pmc_workload.py)
 #   tools/gpu_cycle.sh microbench <out>            build and run tools/microbench/{valu,salu}_bench
 #   tools/gpu_cycle.sh final <out>                 the round's record: pytest -m gpu, the default bench line,
 #                                                  two driver-form lines, a 300-step line, the rocprofv3
@@ -130,6 +132,17 @@ attrib)   # <workload> <samples> <iterations>: per-launch WRITE_SIZE / FETCH_SIZ
     done
     cd "$R" && python3 tools/write_attrib.py fit "$out/$wl/log.json" "$out/$wl/write" "$out/$wl/fetch" \
         > "$out/$wl/fit.txt" && head -8 "$out/$wl/fit.txt" ;;
+wlpmc)   # <workload> <samples> <iterations> <first> <last>
+    wl=$1; ns=$2; it=$3; f0=$4; f1=$5; cd /tmp && export TMPDIR=/tmp
+    for g in sq fetch write; do
+        case $g in sq) ctr="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_BUSY_CYCLES";;
+                   fetch) ctr=FETCH_SIZE;; write) ctr=WRITE_SIZE;; esac
+        timeout -s KILL 120 rocprofv3 --pmc $ctr -d "$R/$out/$g" -o run --output-format csv -- \
+            python3 "$R/tools/pmc_workload.py" run "$wl" "$ns" "$it" "$R/$out/log.json" \
+            > "$R/$out/$g.log" 2>&1 || { tail -5 "$R/$out/$g.log"; exit 1; }
+    done
+    cd "$R" && python3 tools/pmc_workload.py sum "$out" "$f0" "$f1" --json "$out/pmc_${wl}_${ns}.json" \
+        > "$out/summary.txt" && cat "$out/summary.txt" ;;
 microbench)
     for b in valu_bench salu_bench; do
         /opt/rocm/bin/hipcc -O3 --offload-arch=gfx950 "tools/microbench/$b.hip" -o "/tmp/$b" || exit 1
