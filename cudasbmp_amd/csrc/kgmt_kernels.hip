@@ -312,11 +312,13 @@ __global__ __launch_bounds__(1024) void k_fold_r2(KgmtDev d, int tFirst) {
         }
     }
     __syncthreads();
+#ifndef SBMP_FOLD_NOFLUSH   // timing experiment only: the LDS phase alone (wrong results)
     for (int i = threadIdx.x; i < d.nR2; i += blockDim.x) {
         const uint32_t v = sCnt[i];
         if (v & 0xffffu) atomicAdd(&d.R2Valid[i], (int)(v & 0xffffu));
         if (v >> 16) atomicAdd(&d.R2Invalid[i], (int)(v >> 16));
     }
+#endif
 }
 
 // ------------------------------------------------------------------ finish
