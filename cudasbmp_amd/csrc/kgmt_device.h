@@ -111,10 +111,13 @@ constexpr int kRecordF4 = 3;   // sharded record: state, ctrl (a, steer, dur, pa
 // The compact form of the sharded k_step's exchange (k_oneshot, and k_step's own tail
 // when the exchange is fused; kgmt_kernels.hip): u64 offsets and counts of the send
 // buffer, then the compact layout's region starts and total.
-constexpr int kFxCounters = 9;   // fused exchange: 8 arrival shards + the top counter
+constexpr int kFxReplicas = 8;   // fused exchange: arrival counter replicas (one per worker) ...
+constexpr int kFxShards = 8;     // ... each sharded by owned block mod 8
+constexpr int kFxCounters = kFxReplicas * kFxShards;
 constexpr int kFxStride = 32;    // u32 words between counters (128 B)
 struct OneshotCompact {
     int nR1, rowOff, rowWords, cntOff, owned, nBlocks, newOff, newWords;
+    int c16Off;   // u64 offset of the block counts as u16 (the receiver writes them from the block words)
     int cR, cB, cN, total;
 };
 
@@ -230,6 +233,7 @@ struct KgmtDev {
     OneshotCompact xc;
     int listPlain;   // sharded lists readable with plain loads (the mirror, or a local shard group)
     int xRowOff, xCntOff, xNewOff;   // u64 offsets of the row words, block words and R2New bytes
+    int xC16Off;   // u64 offset of the block counts as u16 (global block order; 16-B aligned): k_step's LDS row table
     // k_step reads this struct from device memory (a copy the host refreshes before a
     // launch when it changed): as a 600-B kernel argument its fields were loaded at
     // entry, spilled to VGPR lanes and reloaded, four serial scalar round trips

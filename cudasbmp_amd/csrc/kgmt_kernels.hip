@@ -880,11 +880,18 @@ __device__ __forceinline__ void oneshot_unpack(const OneshotCompact& x, const un
         recv[i < x.cR ? i : x.rowOff + (i - x.cR)] = s;
     } else if (i < x.cN) {   // rank r's owned blocks lb, lb + 1 -> global blocks r + P lb
         int* cnt = reinterpret_cast<int*>(recv + x.cntOff);
+        uint16_t* c16 = reinterpret_cast<uint16_t*>(recv + x.c16Off);   // and the counts alone (k_step's LDS table)
         const int lb = 2 * (i - x.cB);
         for (int r = 0; r < nranks; ++r) {
             const int g0 = r + nranks * lb, g1 = g0 + nranks;
-            if (lb < x.owned && g0 < x.nBlocks) cnt[g0] = (int)(unsigned)v[r];
-            if (lb + 1 < x.owned && g1 < x.nBlocks) cnt[g1] = (int)(unsigned)(v[r] >> 32);
+            if (lb < x.owned && g0 < x.nBlocks) {
+                cnt[g0] = (int)(unsigned)v[r];
+                c16[g0] = (uint16_t)(v[r] & 0xffffu);
+            }
+            if (lb + 1 < x.owned && g1 < x.nBlocks) {
+                cnt[g1] = (int)(unsigned)(v[r] >> 32);
+                c16[g1] = (uint16_t)((v[r] >> 32) & 0xffffu);
+            }
         }
     } else {   // R2New: or of the bits, back to bytes
         unsigned long long bits = 0ull;
@@ -976,48 +983,52 @@ __global__ __launch_bounds__(kBlock) void k_oneshot(OneshotArgs a, const unsigne
 // Every expanding workgroup calls this at its exit.  Its stores that the exchange reads
 // (R1 deltas: agent atomics; row and block words, R2New bytes: sc1 stores) and its list
 // pushes into the mirrors (system scope) have completed (s_waitcnt vmcnt(0) in every
-// wave, then a barrier); lane 0 adds one to the arrival counter of its shard (block
-// index mod 8: 128 arrivals per counter at 1,024 blocks, below one word's atomic rate,
-// where one counter for all would queue; each counter on a line of its own), and the
-// shard's last arrival adds one to the top counter and waits until every shard is in.
-// Those eight workgroups are then the workers: every byte they need is in memory, and
-// worker c reads chunk c of the compact words with sc1 loads (past both caches; per-XCD
-// L2s are not coherent), sends it into the peers' inboxes, raises its flag and waits for
-// theirs (chunk c of k_oneshot's flags, the same sequence numbers), and writes its part
-// of recv, which the next launch reads after the kernel boundary.
+// wave, then a barrier); then one wave instruction with 8 active lanes adds one to each
+// of 8 arrival replicas, each sharded 8 ways (the workgroup's shard: owned block mod 8;
+// every counter on a 128-B line of its own, so a line takes ~128 arrivals, not 1,025; the
+// planner workgroup adds too, step_planner_arrive), and the workgroup leaves unless it is
+// a worker.  The workers are the workgroups of owned blocks 0..7: worker c polls the 8
+// shard counters of replica c (one load per lane) until every workgroup of the launch has
+// added (the guide's replicated, sharded counter hand-off: MI355X_MICROARCH.md, inter-
+// workgroup visibility), so the last arrival's one atomic instruction releases all eight
+// workers.  (Round 4 let each shard's last arrival add to a top counter that the workers
+// polled: one more dependent atomic after the last wave.)
+// Every byte the workers need is then in memory, and worker c reads chunk c of the
+// compact words with sc1 loads (past both caches; per-XCD L2s are not coherent), sends
+// it into the peers' inboxes, raises its flag and waits for theirs (chunk c of
+// k_oneshot's flags, the same sequence numbers), and writes its part of recv, which the
+// next launch reads after the kernel boundary.
 constexpr int kFxRegs = 4;   // compact words a thread keeps between its send and its combine
+// Arrival of one workgroup (shard = its owned block mod 8; the planner counts in shard 0):
+// one instruction, lane r adding to replica r's counter of that shard.
+__device__ __forceinline__ void fx_arrive(const KgmtDev& d, int t, int shard) {
+    SBMP_GAS unsigned* const arr = G(d.xArrive) + (size_t)(t & 1) * kFxCounters * kFxStride;
+    if (threadIdx.x < kFxReplicas)
+        __hip_atomic_fetch_add(arr + (threadIdx.x * kFxShards + shard) * kFxStride, 1u, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+}
 __device__ __forceinline__ void k_step_exchange(const KgmtDev& d, int nranks, int rank, int nRows, int t) {
     const int tid = (int)threadIdx.x;
-    const int nW = min(8, nRows);   // workers: the last arrival of each shard
-    __shared__ int sRole;
-    // each counter on a 128-B line of its own (atomics to one line serialise at the memory side)
-    SBMP_GAS unsigned* const arr = G(d.xArrive) + (size_t)(t & 1) * kFxCounters * kFxStride;
-    if (tid == 0) {
-        const int b = (int)blockIdx.x - 1;
-        const int shard = b & 7;
-        const int expect = (nRows - shard + 7) / 8;
-        const unsigned old =
-            __hip_atomic_fetch_add(arr + shard * kFxStride, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        int role = -1;
-        if ((int)old + 1 == expect) {   // the shard's last arrival: worker `shard`, once every shard is in
-            __hip_atomic_fetch_add(arr + 8 * kFxStride, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
-            // + 1: the planner workgroup's own arrival (step_planner_arrive), after its last read of
-            // recv, which the workers overwrite
-            while ((int)__hip_atomic_load(arr + 8 * kFxStride, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < nW + 1) {
-                if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > kExchangeWaitTicks) {   // report, do not hang
-                    atomicExch(&d.status->error, kErrExchange);
-                    break;
-                }
-                __builtin_amdgcn_s_sleep(1);
+    const int nW = min(kFxReplicas, nRows);   // workers: owned blocks 0 .. nW - 1
+    const int c = (int)blockIdx.x - 1;        // this workgroup's owned block: worker c if c < nW
+    fx_arrive(d, t, c & (kFxShards - 1));
+    if (c >= nW) return;
+    if (tid < kFxShards) {   // lanes 0-7: replica c's shard counters, until every workgroup is in
+        const SBMP_GAS unsigned* const rep = G(d.xArrive) + ((size_t)(t & 1) * kFxCounters + c * kFxShards + tid) * kFxStride;
+        const unsigned want = (unsigned)((nRows - tid + kFxShards - 1) / kFxShards) + (tid == 0 ? 1u : 0u);   // + the planner
+        const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
+        while (true) {
+            const bool in = __hip_atomic_load(rep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= want;
+            if (__ballot(!in) == 0ull) break;   // (lanes 8-63 are inactive here)
+            if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > kExchangeWaitTicks) {   // report, do not hang
+                if (tid == 0) atomicExch(&d.status->error, kErrExchange);
+                break;
             }
-            role = shard;
+            __builtin_amdgcn_s_sleep(1);
         }
-        sRole = role;
     }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // no instruction: the loads below stay below
     __syncthreads();
-    const int c = sRole;
-    if (c < 0) return;
     // diagnostics: worker 0's stamps in k_oneshot's rows of the timeline (tools/timeline.py --step)
     long long* const fxTl =
         (d.timelineFin && t == d.timelineIter && tid == 0) ? d.timelineFin + (size_t)(1 + c) * kTimelineStamps : nullptr;
@@ -1090,14 +1101,12 @@ __device__ __forceinline__ void k_step_exchange(const KgmtDev& d, int nranks, in
 // The planner workgroup of a fused-exchange k_step(t) reads t-1's recv (row, block and
 // delta words, R2New bytes) at entry and, while it inserts t-1's rows, the block words of
 // their rows; the workers of exchange t rewrite recv.  So it arrives too, once its loads
-// have returned (every wave's vmcnt(0), then a barrier): one add to the top counter,
-// which the workers wait for besides the shards' (ADVICE r04).
+// have returned (every wave's vmcnt(0), then a barrier): it adds to the arrival replicas
+// like an expanding workgroup, and the workers wait for it too.
 __device__ __forceinline__ void step_planner_arrive(const KgmtDev& d, int t) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (threadIdx.x == 0)
-        __hip_atomic_fetch_add(G(d.xArrive) + ((size_t)(t & 1) * kFxCounters + 8) * kFxStride, 1u, __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
+    fx_arrive(d, t, 0);
 }
 
 size_t oneshot_inbox_words(long long n, int nranks) { return (size_t)2 * nranks * n + (size_t)nranks * kOneshotChunks; }
@@ -1339,6 +1348,54 @@ __device__ __forceinline__ void row_locate(const ShardView& sv, const int* w, in
     *idx = off;
 }
 
+// The same from the LDS table of u16 block counts (global block order, all rows): a
+// position inside a row without a dependent load of the row's block words.
+__device__ __forceinline__ void row_locate_lds(const ShardView& sv, const uint16_t* sC16, int r, int off, int* block,
+                                               int* idx) {
+    const uint16_t* w = sC16 + (size_t)r * sv.nranks;
+    int q = 0;
+#pragma unroll
+    for (int k = 0; k < kMaxRanks - 1; ++k) {
+        if (k == q && k + 1 < sv.nranks) {
+            const int c = w[k];
+            if (off >= c) {
+                off -= c;
+                q = k + 1;
+            }
+        }
+    }
+    *block = r * sv.nranks + q;
+    *idx = off;
+}
+// Sharded prologue: the exchange's u16 block counts (nBlocks of them, 16-B padded) into
+// LDS, loaded with the first batch (issue) and stored once the scan has waited for it.
+struct C16Load {
+    uint4 v[kMaxRanks / 2];   // 1,024 rows x P u16 over 256 threads: at most 4 x 16 B each
+};
+__device__ __forceinline__ C16Load c16_issue(const KgmtDev& d) {
+    C16Load c;
+    // an exact-size buffer: loads past the table return 0 without a memory access, so every
+    // load is issued unconditionally (no branch, one batch)
+    const int n16 = (d.nBlocks + 7) >> 3;
+    const __amdgpu_buffer_rsrc_t r =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<unsigned long long*>(d.stepXr + d.xC16Off), (short)0, n16 * 16,
+                                          kBufferDword3);
+#pragma unroll
+    for (int u = 0; u < kMaxRanks / 2; ++u) {
+        const sbmp_u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(r, ((int)threadIdx.x + u * kBlock) * 16, 0, 0);
+        c.v[u] = make_uint4(x[0], x[1], x[2], x[3]);
+    }
+    return c;
+}
+__device__ __forceinline__ void c16_store(const KgmtDev& d, const C16Load& c, uint16_t* sC16) {
+    const int n16 = (d.nBlocks + 7) >> 3;
+#pragma unroll
+    for (int u = 0; u < kMaxRanks / 2; ++u) {
+        const int i = (int)threadIdx.x + u * kBlock;
+        if (i < n16) reinterpret_cast<uint4*>(sC16)[i] = c.v[u];
+    }
+}
+
 // jGoal of a sharded scan: the lowest global index of a goal child, in row gRow.
 __device__ __forceinline__ int row_goal(const ShardView& sv, const int* sPfx, int gRow) {
     if (gRow == kNoGoalIdx) return kNoGoalIdx;
@@ -1435,7 +1492,7 @@ __device__ __forceinline__ StepPlan step_plan(const KgmtDev& d, int t, int expan
 // scores and snapshot published as 8-B words tagged with t.
 template <bool SH>
 __device__ __forceinline__ void step_planner(const KgmtDev& d, const ShardView& sv, int t, int expand, int* sPfx,
-                                             int (*sRed)[kBlock / kWave], int* sCovInc, float* sPart) {
+                                             int (*sRed)[kBlock / kWave], int* sCovInc, float* sPart, uint16_t* sC16) {
     constexpr int kW = kMaxR2Words / kBlock;
     const int tid = threadIdx.x;
     const int nW = d.nR2 >> 5;
@@ -1501,8 +1558,10 @@ __device__ __forceinline__ void step_planner(const KgmtDev& d, const ShardView& 
     for (int i = tid; i < d.nR1; i += kBlock) sCovInc[i] = 0;
     int A, jGoal;
     if constexpr (SH) {
+        const C16Load c16 = c16_issue(d);
         int gRow;
         step_scan_rows(sv, pk, sPfx, sRed, &A, &gRow);
+        c16_store(d, c16, sC16);   // read by the inserts, behind the barrier before the scores
         if (gRow != kNoGoalIdx) __syncthreads();   // uniform (rare): row_goal reads sPfx[gRow]
         jGoal = row_goal(sv, sPfx, gRow);
     } else {
@@ -1642,9 +1701,8 @@ __device__ __forceinline__ void step_planner(const KgmtDev& d, const ShardView& 
             for (int step = kMaxStepBlocks / 2; step > 0; step >>= 1)
                 if (lo + step < nS && sPfx[lo + step] <= j) lo += step;
             if constexpr (SH) {
-                int w[kMaxRanks], blk, idx;
-                row_words(sv, lo, w);
-                row_locate(sv, w, lo, j - sPfx[lo], &blk, &idx);
+                int blk, idx;
+                row_locate_lds(sv, sC16, lo, j - sPfx[lo], &blk, &idx);
                 return list_entry<SH>(d, pp, blk, idx);
             } else {
                 return list_entry<SH>(d, pp, lo, j - sPfx[lo]);
@@ -1715,8 +1773,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) voi
     constexpr int kRegObs = obs_in_registers(OBS);
     int* const sPfx = reinterpret_cast<int*>(sDyn + (kLdsObs ? d.nObs : 0));
     uint32_t* const sNew = reinterpret_cast<uint32_t*>(sPfx + (SH ? sv.nRows : d.nBlocks) + 1);
+    // sharded: the u16 block counts of every row, 16-B aligned after the R2New bits (step_lds_bytes)
+    uint16_t* const sC16 = reinterpret_cast<uint16_t*>(sPfx + ((((SH ? sv.nRows : d.nBlocks) + 1 + (d.nR2 >> 5)) + 3) & ~3));
     if (blockIdx.x == 0) {
-        step_planner<SH>(d, sv, t, expand, sPfx, sRed, sCovInc, sPart);
+        step_planner<SH>(d, sv, t, expand, sPfx, sRed, sCovInc, sPart, sC16);
         if constexpr (SH) {
             if (expand && d.fusedX) step_planner_arrive(d, t);
         }
@@ -1762,8 +1822,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) voi
     // waiting scalar load would serialise behind the scan)
     const int4 pk = G(cnt4)[tid];
     const IterCtrl pc = *ctrlP;
-    int rowW[SH ? kMaxRanks : 1];   // sharded: the block words of this workgroup's row (its inserts)
-    if constexpr (SH) row_words(sv, b, rowW);
+    C16Load c16;   // sharded: the u16 block counts of every row (row positions, inserts)
+    if constexpr (SH) c16 = c16_issue(d);
     const int goalIdx = statusP->goalIdx;
     const uint4 ra = rngAP[slot];
     const uint2 rb = rngBP[slot];
@@ -1800,6 +1860,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) voi
         if constexpr (SH) {
             int gRow;
             step_scan_rows(sv, pk, sPfx, sRed, &A, &gRow);
+            c16_store(d, c16, sC16);   // published by the plan's barrier below
             if (gRow != kNoGoalIdx) __syncthreads();   // uniform (rare): row_goal reads sPfx[gRow]
             jGoal = row_goal(sv, sPfx, gRow);
         } else {
@@ -1879,7 +1940,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) voi
                     const int j = j0 + o, dst = q.tsPrev + j;
                     if (j < q.nIns && dst < d.M) {   // D13: the reference writes past M here
                         int blk, idx;
-                        row_locate(sv, rowW, b, o, &blk, &idx);
+                        row_locate_lds(sv, sC16, b, o, &blk, &idx);
                         const SBMP_GAS float4* e = list_entry<SH>(d, pp, blk, idx);
                         const float4 s4 = list_load<SH>(d, e);
                         const float4 u4 = list_load<SH>(d, e + 1);
@@ -1951,10 +2012,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) voi
                 while (lo + 1 < nS && sPfx[lo + 1] <= j) ++lo;
         }
         if (fromList) {
-            if constexpr (SH) {   // the row's blocks: one more (L2) round trip for their words
-                int w[kMaxRanks], blk, idx;
-                row_words(sv, lo, w);
-                row_locate(sv, w, lo, j - sPfx[lo], &blk, &idx);
+            if constexpr (SH) {   // the row's blocks: from the LDS table (round 4: one more L2 round trip)
+                int blk, idx;
+                row_locate_lds(sv, sC16, lo, j - sPfx[lo], &blk, &idx);
                 src = list_entry<SH>(d, pp, blk, idx);
             } else {
                 src = list_entry<SH>(d, pp, lo, j - sPfx[lo]);
@@ -1983,7 +2043,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) voi
     }
     // the grid index's cell-start table into LDS: every row lookup of the Euler loop is
     // then an LDS read instead of an L2 round trip (the boxes stay in global memory)
-    int* const sGridStart = reinterpret_cast<int*>(sNew + nW);
+    int* const sGridStart = SH ? reinterpret_cast<int*>(sC16 + ((d.nBlocks + 7) & ~7)) : reinterpret_cast<int*>(sNew + nW);
     if constexpr (OBS == kObsGrid) {
         const int nStart = d.gridG * d.gridG + 1;
         const SBMP_GAS int* const gs = G(d.gridStart);
@@ -2203,6 +2263,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) voi
             __hip_atomic_store(reinterpret_cast<SBMP_GAS int*>(G(d.stepXs[cp]) + d.xRowOff) + b,
                                (c0 + c1 + c2 + c3) | ((gmin == kNoGoalIdx ? 0 : 1) << 16), __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_AGENT);
+            // the count again as u16 (the summed exchange forms carry it; the compact one rebuilds it)
+            store_wt(reinterpret_cast<uint16_t*>(d.stepXs[cp] + d.xC16Off), gb, (uint16_t)(c0 + c1 + c2 + c3));
         }
         else store_wt(d.stepCnt, cp * kMaxStepBlocks + b, cw);
     }
@@ -2430,12 +2492,22 @@ void launch_expand(const KgmtDev& d, int t, int agent, int blocks, int variant, 
     else launch_expand_agent<1>(d, t, blocks, variant, s, tm);
 }
 
+// k_step's dynamic LDS past the obstacle list: the block (row) prefix and the R2New bits;
+// on a sharded rank also the u16 block counts of every row, 16-B aligned (the kernel's
+// sC16 / sGridStart layout).
+static size_t step_lds_bytes(const KgmtDev& d, bool sh) {
+    const size_t nS = sh ? d.nBlocks / d.nranks : d.nBlocks;   // scan entries: blocks, or rows
+    size_t b = sizeof(int) * (nS + 1) + sizeof(uint32_t) * (size_t)(d.nR2 / 32);
+    if (sh) b = ((b + 15) & ~(size_t)15) + sizeof(uint16_t) * (((size_t)d.nBlocks + 7) & ~(size_t)7);
+    return b;
+}
+
 template <int AGENT, bool SH>
 static void launch_step_form(const KgmtDev& d, int t, int expand, int variant, hipStream_t s,
                              const KernelTiming& tm) {
     // dynamic LDS: [LDS obstacles][block prefix: nBlocks + 1 ints][R2New bits: nR2 / 32 words]
-    const size_t nS = SH ? d.nBlocks / d.nranks : d.nBlocks;   // scan entries: blocks, or rows
-    const size_t pfx = sizeof(int) * (nS + 1) + sizeof(uint32_t) * (size_t)(d.nR2 / 32);
+    // (sharded: [16-B aligned u16 block counts]) [grid cell starts]
+    const size_t pfx = step_lds_bytes(d, SH);
     const size_t shm = sizeof(float4) * (size_t)d.nObs + pfx;   // LDS obstacle forms
     const size_t gridLds = d.gridStart ? sizeof(int) * ((size_t)d.gridG * d.gridG + 1) : 0;   // + the cell starts
     const int blocks = SH ? d.nBlocks / d.nranks : d.nBlocks;
@@ -2477,8 +2549,7 @@ using StepFn = void (*)(const KgmtDev*, int, int, const int4*, const IterCtrl*, 
                         const unsigned long long*, const PlannerStatus*, long long*, int, const int*);
 template <int AGENT, bool SH>
 static StepFn step_fn(const KgmtDev& d, int variant, size_t* shm) {
-    const size_t nS = SH ? d.nBlocks / d.nranks : d.nBlocks;
-    const size_t pfx = sizeof(int) * (nS + 1) + sizeof(uint32_t) * (size_t)(d.nR2 / 32);
+    const size_t pfx = step_lds_bytes(d, SH);
     *shm = pfx;
     if (d.gridStart) {
         *shm = pfx + sizeof(int) * ((size_t)d.gridG * d.gridG + 1);   // + the cell-start table (k_step stages it)
@@ -2556,6 +2627,7 @@ OneshotCompact oneshot_compact(const OneshotLayout& l) {
     x.owned = l.owned;
     x.nBlocks = l.nBlocks;
     x.newOff = l.newOff;
+    x.c16Off = l.c16Off;
     x.newWords = l.newWords;
     x.cR = x.nR1;
     x.cB = x.cR + x.rowWords;

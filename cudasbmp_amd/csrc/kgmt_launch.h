@@ -64,6 +64,7 @@ struct OneshotLayout {
     int rowOff, rows;         // u64 offset of the row words, rows (ints)
     int cntOff, owned, nBlocks;   // u64 offset of the block words (ints), owned blocks, global blocks
     int newOff, newWords;     // u64 offset and words of the R2New bytes
+    int c16Off;               // u64 offset of the u16 block counts (written by the receiver)
 };
 OneshotCompact oneshot_compact(const OneshotLayout& l);   // the compact layout of l
 // tl: diagnostics, 8 stamps per workgroup, or null.

@@ -199,9 +199,13 @@ KgmtPlanner::KgmtPlanner(const sbmp_kgmt_params& p, int nranks, int rank, Exchan
         const size_t dWords = round_up((long long)kDeltaReps * d.nR1, 2);
         const size_t bcWords = round_up(d.nBlocks, 4) / 2, r2Words = round_up(d.nR2, 16) / 8;
         const size_t pfxWords = round_up(d.nBlocks + 1, 4) / 2, totWords = kMaxRanks / 2;
+        // sharded k_step: the block counts again as u16 (owner-written like the block words), so
+        // that every workgroup holds the whole table in LDS and locates a position inside a row
+        // without a dependent load
+        const size_t c16Words = shStep_ ? round_up(d.nBlocks, 8) / 4 : 0;
         unsigned long long* local = nullptr;
         if (shStep_) {
-            xWords_ = dWords + rowWords + bcWords + r2Words;
+            xWords_ = dWords + rowWords + bcWords + c16Words + r2Words;
             local = alloc<unsigned long long>(bcWords + (size_t)nWords);
             localWords_ = bcWords + (size_t)nWords;
             local_ = local;
@@ -223,7 +227,8 @@ KgmtPlanner::KgmtPlanner(const sbmp_kgmt_params& p, int nranks, int rank, Exchan
         d.listPlain = (sharded && !ex) ? 1 : 0;   // a local group: every rank's buffers are this GPU's
         d.xRowOff = (int)dWords;
         d.xCntOff = (int)(dWords + rowWords);
-        d.xNewOff = (int)(dWords + rowWords + bcWords);
+        d.xC16Off = (int)(dWords + rowWords + bcWords);
+        d.xNewOff = (int)(dWords + rowWords + bcWords + c16Words);
         int* bc = reinterpret_cast<int*>(sharded ? local : xSend_ + dWords);
         unsigned long long* gn = sharded ? local + bcWords : xSend_ + dWords + bcWords;
         d.blockCountOut = bc;
@@ -388,6 +393,7 @@ KgmtPlanner::KgmtPlanner(const sbmp_kgmt_params& p, int nranks, int rank, Exchan
             l.nBlocks = d.nBlocks;
             l.newOff = d.xNewOff;
             l.newWords = (int)xWords_ - d.xNewOff;
+            l.c16Off = d.xC16Off;
             d.xc = oneshot_compact(l);
             if (d.xc.total > (int)xWords_) d.fusedX = 0;   // cannot happen (compact is smaller)
         }
@@ -756,6 +762,7 @@ void KgmtPlanner::stage_exchange(int t) {
             cx.nBlocks = d_.nBlocks;
             cx.newOff = d_.xNewOff;
             cx.newWords = (int)xWords_ - d_.xNewOff;
+            cx.c16Off = d_.xC16Off;
         }
         long long* tl = (d_.timelineFin && t == d_.timelineIter) ? d_.timelineFin + kTimelineStamps : nullptr;
         launch_oneshot(inbox_, send, xRecv_, (long long)xWords_, d_.nranks, d_.rank, xSeq_, &d_.status->error,
