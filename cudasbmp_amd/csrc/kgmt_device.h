@@ -222,9 +222,9 @@ struct KgmtDev {
     // Fused exchange (sharded k_step + one-shot exchange + list mirror): the last
     // expanding workgroup of k_step(t) runs the exchange of t itself (k_step_exchange),
     // instead of a k_oneshot launch.  xInbox: every rank's inbox, mapped here;
-    // xArrive: [2 parities][kFxCounters][kFxStride] arrival counters (8 shards by block
-    // index, then the top counter, each on a 128-B line); exchange t has sequence number
-    // xSeqBase + t.
+    // xArrive: [2 parities][kFxReplicas][kFxShards][kFxStride] arrival counters (replica r
+    // polled by worker r, shard = owned block mod 8, each on a 128-B line); exchange t has
+    // sequence number xSeqBase + t.
     int fusedX;
     int xInboxWords;   // n of the inbox layout (slot stride)
     unsigned long long* xInbox[kMaxRanks];
