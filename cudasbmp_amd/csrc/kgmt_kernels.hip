@@ -291,34 +291,104 @@ __global__ __launch_bounds__(kBlock) void k_expand(KgmtDev d, int t) {
 // overflows), flushed with one atomic per nonzero half, consecutive lanes on
 // consecutive cells.  Keys of slots >= S of that iteration are stale and skipped;
 // iterations that did not execute are skipped whole.
-__global__ __launch_bounds__(1024) void k_fold_r2(KgmtDev d, int tFirst) {
-    extern __shared__ uint32_t sCnt[];
+// Where the time goes (round 5, -DSBMP_TIMELINE stamps, tools/fold_timeline.py): the
+// adds are VALU-bound, not LDS-bound (64 keys per thread, 16 waves per CU; at ~10 VALU
+// per key the adds took 3-4.5 us, against ~1 us of LDS time at the random-word rate of
+// tools/microbench/lds_atomic_bench), so each key is now 5 VALU: the cell and the
+// increment by shifts, masks and one multiply-add, and the skipped keys (kNoKey, or a
+// slot >= S, which the rare piece that straddles S turns into kNoKey) sent by one min
+// to a per-lane sink word past the histogram: no branch, no compare per key.  All of a
+// thread's key loads issue at entry (one round trip, not one per 16 B) and the
+// histogram is cleared while the control block's scalar load is in flight.
+constexpr int kFoldThreads = 1024;
+constexpr int kFoldLoads = (kFoldKeys + 8 * kFoldThreads - 1) / (8 * kFoldThreads);   // 16-B pieces per thread
+// The histogram is the kernel's only LDS (dynamic, so at LDS address 0): the add takes
+// the byte offset itself (the compiler added the base, 0, in one more VALU per key).
+// Its completion is waited for explicitly before the barrier that ends the adds.
+__device__ __forceinline__ void fold_add(uint32_t key, uint32_t sinkB) {
+    // byte offset of cell (key & 0x7fff), or the sink for kNoKey (cell 0x7fff >= nR2)
+    const uint32_t a = __builtin_elementwise_min((key & 0x7fffu) << 2, sinkB);
+    const uint32_t valid = key >> 15;   // 0 or 1
+    const uint32_t inc = 0x10000u - valid * 0xffffu;   // valid: 1, invalid: 1 << 16
+    asm volatile("ds_add_u32 %0, %1" : : "v"(a), "v"(inc) : "memory");
+}
+__global__ __launch_bounds__(kFoldThreads) void k_fold_r2(KgmtDev d, int tFirst, int keysPerGroup) {
+    extern __shared__ uint32_t sCnt[];   // nR2 cells, then kWave sink words
+    const int tid = (int)threadIdx.x;
     const int t = tFirst + (int)blockIdx.y;
-    const IterCtrl c = d.ctrl[t];
-    if (!c.executed) return;
-    for (int i = threadIdx.x; i < d.nR2; i += blockDim.x) sCnt[i] = 0u;
-    __syncthreads();
     const uint16_t* row = d.r2log + (size_t)(t % kFoldEvery) * d.logSlots;
-    const int begin = (int)blockIdx.x * kFoldKeys;
-    const int end = min(begin + kFoldKeys, d.logSlots);
-    for (int i = begin + (int)threadIdx.x * 8; i < end; i += (int)blockDim.x * 8) {
-        const uint4 w = *reinterpret_cast<const uint4*>(row + i);
-        const uint32_t wv[4] = {w.x, w.y, w.z, w.w};
-        const int gslot = (d.rank + d.nranks * (i >> 8)) * kBlock + (i & (kBlock - 1));   // 8 keys, one block
+    const int begin = (int)blockIdx.x * keysPerGroup;
+    const int end = min(begin + keysPerGroup, d.logSlots);
+    uint4 w[kFoldLoads];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            const uint32_t key = (wv[j >> 1] >> ((j & 1) * 16)) & 0xffffu;
-            if (gslot + j < c.S && key != kNoKey) atomicAdd(&sCnt[key & 0x7fffu], (key & 0x8000u) ? 1u : 0x10000u);
-        }
+    for (int u = 0; u < kFoldLoads; ++u) {
+        const int i = begin + (tid + u * kFoldThreads) * 8;
+        w[u] = (i < end) ? *reinterpret_cast<const uint4*>(row + i) : make_uint4(~0u, ~0u, ~0u, ~0u);
     }
+#ifdef SBMP_TIMELINE   // diagnostics (tools/fold_timeline.py): the fold of iteration timelineIter, wave by wave
+    long long* const ftl = (d.timelineFin && t == d.timelineIter && (tid & (kWave - 1)) == 0)
+                               ? d.timelineFin + ((size_t)blockIdx.x * (kFoldThreads / kWave) + (tid >> 6)) * kTimelineStamps
+                               : nullptr;
+#define SBMP_FSTAMP(k) do { if (ftl) ftl[k] = (long long)__builtin_amdgcn_s_memrealtime(); } while (0)
+#else
+#define SBMP_FSTAMP(k) do { } while (0)
+#endif
+    SBMP_FSTAMP(0);
+    const IterCtrl c = d.ctrl[t];   // (the clear below overlaps its round trip)
+    const int nR2 = d.nR2;
+    for (int i = tid; i < nR2 + kWave; i += kFoldThreads) sCnt[i] = 0u;
+    if (!c.executed) return;   // uniform
+    SBMP_FSTAMP(1);
     __syncthreads();
-#ifndef SBMP_FOLD_NOFLUSH   // timing experiment only: the LDS phase alone (wrong results)
-    for (int i = threadIdx.x; i < d.nR2; i += blockDim.x) {
-        const uint32_t v = sCnt[i];
-        if (v & 0xffffu) atomicAdd(&d.R2Valid[i], (int)(v & 0xffffu));
-        if (v >> 16) atomicAdd(&d.R2Invalid[i], (int)(v >> 16));
+    SBMP_FSTAMP(2);
+#ifdef SBMP_TIMELINE
+    if (ftl) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        SBMP_FSTAMP(3);
     }
 #endif
+    const uint32_t sinkB = (uint32_t)(nR2 + (tid & (kWave - 1))) * 4u;
+#pragma unroll
+    for (int u = 0; u < kFoldLoads; ++u) {
+        const int i = begin + (tid + u * kFoldThreads) * 8;
+        const int live = c.S - (d.rank + d.nranks * (i >> 8)) * kBlock - (i & (kBlock - 1));   // keys of slots < S
+        uint32_t kw[4] = {w[u].x, w[u].y, w[u].z, w[u].w};
+        if (live < 8) {   // the piece that straddles S (or lies past it): its stale keys become kNoKey
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                kw[k] |= (2 * k >= live ? 0xffffu : 0u) | (2 * k + 1 >= live ? 0xffff0000u : 0u);
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            fold_add(kw[k] & 0xffffu, sinkB);
+            fold_add(kw[k] >> 16, sinkB);
+        }
+    }
+    SBMP_FSTAMP(4);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the adds (inline asm: not tracked)
+    __syncthreads();
+    SBMP_FSTAMP(5);
+    for (int i0 = tid; i0 < nR2; i0 += 8 * kFoldThreads) {   // 8 cells read, then their atomics
+        uint32_t v[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) v[q] = (i0 + q * kFoldThreads < nR2) ? sCnt[i0 + q * kFoldThreads] : 0u;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            if (v[q] & 0xffffu) atomicAdd(&d.R2Valid[i0 + q * kFoldThreads], (int)(v[q] & 0xffffu));
+            if (v[q] >> 16) atomicAdd(&d.R2Invalid[i0 + q * kFoldThreads], (int)(v[q] >> 16));
+        }
+    }
+#ifdef SBMP_TIMELINE
+    if (ftl) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        SBMP_FSTAMP(6);
+        unsigned hw, xcc;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+        ftl[7] = ((long long)xcc << 32) | hw;
+    }
+#endif
+#undef SBMP_FSTAMP
 }
 
 // ------------------------------------------------------------------ finish
@@ -2610,12 +2680,16 @@ void launch_step(const KgmtDev& d, int t, int expand, int agent, int variant, hi
 
 void launch_fold_r2(const KgmtDev& d, int tFirst, int tLast, hipStream_t s, const KernelTiming& tm) {
     if (!d.r2log || tLast < tFirst) return;
-    const size_t shm = sizeof(uint32_t) * (size_t)d.nR2;
-    if (shm > 65536)   // dynamic LDS above 64 KB needs the opt-in (n > 8); per device, so every time
+    const size_t shm = sizeof(uint32_t) * ((size_t)d.nR2 + kWave);
+    if (shm > 65536)   // dynamic LDS above 64 KB needs the opt-in; per device, so every time
         (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_fold_r2),
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
-    const dim3 grid((d.logSlots + kFoldKeys - 1) / kFoldKeys, tLast - tFirst + 1);
-    launch(k_fold_r2, grid, dim3(1024), shm, s, tm, d, tFirst);
+    // the iteration's keys split evenly (whole 8-key loads) over the fewest workgroups of
+    // at most kFoldKeys each
+    const int groups = (d.logSlots + kFoldKeys - 1) / kFoldKeys;
+    const int per = (((d.logSlots + groups - 1) / groups) + 7) & ~7;
+    const dim3 grid(groups, tLast - tFirst + 1);
+    launch(k_fold_r2, grid, dim3(kFoldThreads), shm, s, tm, d, tFirst, per);
 }
 
 OneshotCompact oneshot_compact(const OneshotLayout& l) {

@@ -21,7 +21,8 @@ def host_rank():
     os.environ.setdefault("MASTER_PORT", "29534")
     import torch.distributed as dist
     from cudasbmp_amd.host_comm import TorchCollectives
-    dist.init_process_group("gloo", rank=0, world_size=1)
+    if not dist.is_initialized():
+        dist.init_process_group("gloo", rank=0, world_size=1)
     return (TorchCollectives(dist), 1, 0)
 
 
