@@ -115,7 +115,7 @@ final)
     timeout -k 10 200 python3 bench.py --steps 300 --warmup 20 --no-cpu-baseline --no-ttfs > "$R/$out/s300.json" \
         2> "$R/$out/s300.err" || exit 1
     line "$R/$out/s300.json" s300
-    timeout -k 10 300 python3 bench.py --workload c5 --samples-per-gpu 131072 --no-cpu-baseline --no-ttfs \
+    timeout -k 10 300 python3 bench.py --workload c5 --samples-per-gpu 131072 --warmup 5 --steps 35 --no-cpu-baseline --no-ttfs \
         > "$R/$out/c5_131k.json" 2> "$R/$out/c5_131k.err" || exit 1
     line "$R/$out/c5_131k.json" c5_131k
     cd /tmp && export TMPDIR=/tmp
