@@ -326,9 +326,10 @@ __global__ __launch_bounds__(kFoldThreads) void k_fold_r2(KgmtDev d, int tFirst,
         w[u] = (i < end) ? *reinterpret_cast<const uint4*>(row + i) : make_uint4(~0u, ~0u, ~0u, ~0u);
     }
 #ifdef SBMP_TIMELINE   // diagnostics (tools/fold_timeline.py): the fold of iteration timelineIter, wave by wave
-    long long* const ftl = (d.timelineFin && t == d.timelineIter && (tid & (kWave - 1)) == 0)
-                               ? d.timelineFin + ((size_t)blockIdx.x * (kFoldThreads / kWave) + (tid >> 6)) * kTimelineStamps
-                               : nullptr;
+    // rows 9.. of the k_step stamp rows (0: planner, 1-8: exchange workers), where they fit
+    const int ftlRow = 9 + (int)blockIdx.x * (kFoldThreads / kWave) + (tid >> 6);
+    long long* const ftl = (d.timelineFin && t == d.timelineIter && (tid & (kWave - 1)) == 0 && ftlRow < 1 + d.nBlocks)
+                               ? d.timelineFin + (size_t)ftlRow * kTimelineStamps : nullptr;
 #define SBMP_FSTAMP(k) do { if (ftl) ftl[k] = (long long)__builtin_amdgcn_s_memrealtime(); } while (0)
 #else
 #define SBMP_FSTAMP(k) do { } while (0)

@@ -15,7 +15,7 @@ NAMES = ["entry", "clear", "barrier1", "keys", "adds", "barrier2", "flush"]
 
 
 def main():
-    a = np.fromfile(sys.argv[1], dtype=np.int64).reshape(-1, 8)
+    a = np.fromfile(sys.argv[1], dtype=np.int64).reshape(-1, 8)[9:]   # rows 0-8: k_step's planner and exchange
     live = a[:, 6] != 0
     a = a[live]
     t0 = a[:, 0].min()
