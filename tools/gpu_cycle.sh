@@ -72,7 +72,7 @@ timeline)
     for it in "$@"; do
         (cd "$dir" && SBMP_TIMELINE_ITER=$it SBMP_TIMELINE_OUT="$R/$out/it$it.bin" timeout -k 10 120 python3 bench.py \
             --no-cpu-baseline --no-ttfs --steps 30 --warmup 20 > "$R/$out/b$it.json" 2> "$R/$out/b$it.err") || exit 1
-        python3 tools/timeline.py "$R/$out/it$it.bin" > "$R/$out/k_step_iter$it.txt" && head -30 "$R/$out/k_step_iter$it.txt"
+        python3 tools/timeline.py "$R/$out/it$it.bin" --step > "$R/$out/k_step_iter$it.txt" && head -30 "$R/$out/k_step_iter$it.txt"
     done ;;
 sq)
     cd /tmp && export TMPDIR=/tmp
