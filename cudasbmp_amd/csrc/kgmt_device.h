@@ -646,19 +646,12 @@ __device__ __forceinline__ bool motion_valid_culled(float minx, float miny, floa
 //     where the four compares and their mask ANDs / ORs ran on the SALU and the
 //     short-circuit OR had become branches.
 //   - A batch loads kGridBatch consecutive rows unconditionally (the box array holds
-//     kGridBatch padding rows past its end) at immediate offsets from one address, and
-//     masks the rows past the cell run, instead of clamping each index.
+//     kGridBatch never-met padding rows past its end) at immediate offsets from one
+//     address, and tests them all: rows past the cell run are other cells' boxes, which
+//     cannot change the answer (grid_run_sep), instead of clamping each index.
 //   - Cells by fmed3 (segments are finite: grid_cell's NaN case cannot arise).
 constexpr int kGridBatch = 8;   // boxes loaded per round trip; also the padding rows of gridBoxes
 
-// keep ? v : +inf as one v_cndmask on a lane mask: written as a C select, the compiler
-// sank each padded box's loads and tests into a branch of its own.
-__device__ __forceinline__ float keep_or_inf(bool keep, float v) {
-    const unsigned long long m = __ballot(keep);
-    float r;
-    asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "v"(__builtin_inff()), "v"(v), "s"(m));
-    return r;
-}
 // The segment's cell span and the start offsets of its first two cell rows (grid_run_sep
 // tests their boxes).
 struct GridRun {
@@ -717,7 +710,11 @@ __device__ __forceinline__ float grid_run_sep(GridRun q, float minx, float miny,
                     const sbmp_f32x2 lo = sbmp_f32x2{o[k].x, o[k].y} - mx;
                     const sbmp_f32x2 hi = mn - sbmp_f32x2{o[k].z, o[k].w};
                     const float sk = __builtin_fmaxf(vmax3(lo.x, lo.y, hi.x), hi.y);
-                    sep = seg_min(sep, keep_or_inf(i + k < e, sk));   // rows past the run test nothing
+                    // Rows past the run are tested too, unmasked: they are other cells' boxes (or the
+                    // never-met padding rows), and a box that meets the segment is listed in one of
+                    // the segment's cells (obstacle_grid.h), so the answer (some box meets it) is the
+                    // same; the mask cost a ballot and a select per row.
+                    sep = seg_min(sep, sk);
                 }
             }
         }

@@ -669,7 +669,8 @@ void KgmtPlanner::build_grid(const float* d_obstacles, int nObs) {
         // cells a side (32 KB); any G gives the same answers, a coarser one more boxes per cell
         const HostObstacleGrid g =
             build_obstacle_grid(h.data(), nObs, d.width, d.height, std::min(grid_resolution(nObs), kMaxLdsGridG));
-        // kGridBatch zeroed rows past the end: grid_free_fast loads whole batches
+        // kGridBatch rows past the end that no segment meets ((+inf, +inf) - (-inf, -inf): the
+        // separation metric is +inf): grid_free_fast loads and tests whole batches
         const size_t nStart = g.start.size(), nBoxes = g.boxes.size() + kGridBatch;
         if (nStart > gridStartCap_) {
             if (gridStart_) SBMP_HIP(hipFree(gridStart_));
@@ -684,9 +685,9 @@ void KgmtPlanner::build_grid(const float* d_obstacles, int nObs) {
             gridBoxesCap_ = nBoxes;
         }
         SBMP_HIP(hipMemcpy(gridStart_, g.start.data(), sizeof(int) * nStart, hipMemcpyHostToDevice));
-        SBMP_HIP(hipMemset(gridBoxes_, 0, sizeof(float4) * nBoxes));
-        if (!g.boxes.empty())
-            SBMP_HIP(hipMemcpy(gridBoxes_, g.boxes.data(), sizeof(float4) * g.boxes.size(), hipMemcpyHostToDevice));
+        std::vector<float4> rows(nBoxes, make_float4(INFINITY, INFINITY, -INFINITY, -INFINITY));
+        if (!g.boxes.empty()) std::memcpy(rows.data(), g.boxes.data(), sizeof(float4) * g.boxes.size());
+        SBMP_HIP(hipMemcpy(gridBoxes_, rows.data(), sizeof(float4) * nBoxes, hipMemcpyHostToDevice));
         for (float v : h)   // grid_free_fast's separation metric needs boxes without NaN
             if (std::isnan(v)) d.obsNaN = 1;
         d.gridG = g.g;
