@@ -650,7 +650,10 @@ __device__ __forceinline__ bool motion_valid_culled(float minx, float miny, floa
 //     address, and tests them all: rows past the cell run are other cells' boxes, which
 //     cannot change the answer (grid_run_sep), instead of clamping each index.
 //   - Cells by fmed3 (segments are finite: grid_cell's NaN case cannot arise).
-constexpr int kGridBatch = 8;   // boxes loaded per round trip; also the padding rows of gridBoxes
+#ifndef SBMP_GRID_BATCH
+#define SBMP_GRID_BATCH 8
+#endif
+constexpr int kGridBatch = SBMP_GRID_BATCH;   // boxes loaded per round trip; also the padding rows of gridBoxes
 
 // The segment's cell span and the start offsets of its first two cell rows (grid_run_sep
 // tests their boxes).
