@@ -237,6 +237,9 @@ struct KgmtDev {
     // k_step reads this struct from device memory (a copy the host refreshes before a
     // launch when it changed): as a 600-B kernel argument its fields were loaded at
     // entry, spilled to VGPR lanes and reloaded, four serial scalar round trips
+    // Single rank: pinned host word the planner workgroup of every k_step stores
+    // t << 2 | (loop ended) << 1 | (goal found) into (KgmtPlanner::run_to_goal), else null.
+    unsigned long long* hostPoll;
     const KgmtDev* devSelf;
 };
 

@@ -1759,6 +1759,10 @@ __device__ __forceinline__ void step_planner(const KgmtDev& d, const ShardView& 
         st_ctrl(d.ctrl, t, c);
         if (t > 1) store_wt(reinterpret_cast<int*>(d.ctrl + (t - 1)), 9, A);   // .A
         if (q.newGoal != goalIdx) store_wt(reinterpret_cast<int*>(d.status), 0, q.newGoal);   // .goalIdx
+        if (d.hostPoll)   // the host's plan loop: this launch planned t (a vector store over PCIe)
+            __hip_atomic_store(G(d.hostPoll),
+                               ((unsigned long long)t << 2) | (q.runT ? 0ull : 2ull) | (q.newGoal != kNoGoal ? 1ull : 0ull),
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
     // Insert t-1's flagged children (rows tsPrev + j, KGMT.cu:540-593) when they are
     // few: everything above is what the expanders wait for, and from here on this

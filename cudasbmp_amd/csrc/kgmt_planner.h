@@ -55,6 +55,9 @@ public:
     virtual void rank_barrier() {}   // sharded ranks: all ranks reach this point (Exchange::barrier)
     virtual void result(sbmp_plan_result* r) = 0;
     void run(int pollEvery);     // enqueue until the loop ends
+    // plan(): run() with the planner's own loop control (a single k_step rank: the host
+    // watches a pinned word instead of polling with stream synchronisations)
+    virtual void run_plan() { run(8); }
     // Per-iteration dumps (reference KGMT.cu:263-290, commented out there; read by
     // visualization/visualizationKGMT_Steps.m): with a directory set, run() steps one
     // iteration at a time and writes <dir>/Data/<Kind>/<kind><itr>.csv after each.
@@ -119,6 +122,7 @@ public:
         if (ex_) ex_->barrier(stream_);
     }
     void result(sbmp_plan_result* r) override;
+    void run_plan() override;
 
     hipStream_t stream() const override { return stream_; }
     int num_slots() const override { return d_.nSlots; }
@@ -190,8 +194,12 @@ private:
     struct PollBuf {
         IterCtrl ctrl;
         PlannerStatus status;
+        unsigned long long word;   // KgmtDev::hostPoll (single rank)
     };
     PollBuf* poll_ = nullptr;
+    void run_to_goal();                   // run_plan() for a single k_step rank
+    std::vector<hipEvent_t> planEvents_;  // run_to_goal: one per iteration in flight (a ring)
+    bool wallFixed_ = false;              // wallMs_ was taken at the goal iteration's end
     bool flushed_ = true;     // k_step mode: the last enqueued iteration has been inserted
     int lastFolded_ = 0;      // iterations <= lastFolded_ are in R2Valid / R2Invalid
     unsigned long long* local_ = nullptr;   // sharded: the owner's block counts + GNew words

@@ -218,9 +218,9 @@ sbmp_status sbmp_kgmt_plan(sbmp_kgmt* h, const float initial[7], const float goa
     return guarded([&] {
         PLANNER(h);
         P.begin(initial, goal, d_obstacles, obstaclesCount, seed);
-        // Poll every 8 iterations: the kernels of a finished loop are no-ops, so
-        // over-enqueueing costs a few microseconds, not correctness.
-        P.run(8);
+        // The planner's loop control (KgmtPlanner::run_plan): over-enqueued iterations of a
+        // finished loop are no-ops, so they cost a few microseconds, not correctness.
+        P.run_plan();
         if (result) P.result(result);
     });
 }
