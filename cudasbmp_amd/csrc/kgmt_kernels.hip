@@ -1958,6 +1958,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) voi
         }
         __syncthreads();
         q = uniform_plan(sPlan);
+#ifdef SBMP_TL_PROLOGUE   // diagnostics: stamp 4 = after the plan's barrier (instead of the hand-off)
+        SBMP_STAMP(4);
+#endif
     }
     // the fused exchange's arrival (every exit of an expanding workgroup)
     auto fx_exit = [&]() {
@@ -2097,6 +2100,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) voi
             srcCost = reinterpret_cast<const SBMP_GAS float*>(src + 2);
         }
     }
+#ifdef SBMP_TL_PROLOGUE   // stamp 5 = parent located (instead of the epilogue barrier)
+    SBMP_STAMP(5);
+#endif
     // Parent and obstacles are issued back to back and waited for together.
     float4 p;
     float parentCost;
@@ -2231,7 +2237,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) voi
         accept = (u <= __uint_as_float((uint32_t)sw)) || !r2Avail;
         if (!r2Avail) atomicOr(&sNew[q2 >> 5], bit);
     }
+#ifndef SBMP_TL_PROLOGUE
     SBMP_STAMP(4);
+#endif
     const unsigned long long mask = __ballot(accept);
     const unsigned long long word0 =   // lane 0's word
         ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)(word >> 32), 0) << 32) |
@@ -2259,7 +2267,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) voi
         sWaveGoal[wave] = glW;
     }
     __syncthreads();
+#ifndef SBMP_TL_PROLOGUE
     SBMP_STAMP(5);
+#endif
     const int c0 = sWaveCnt[0], c1 = sWaveCnt[1], c2 = sWaveCnt[2], c3 = sWaveCnt[3];
     const int waveOff = (wave > 0 ? c0 : 0) + (wave > 1 ? c1 : 0) + (wave > 2 ? c2 : 0);
     if (flagged) {

@@ -15,6 +15,8 @@ import numpy as np
 NAMES = ["entry", "prologue", "propagate", "accept+store", "count_regions", "barrier", "flush"]
 # k_step (SBMP_STEP=1, the default on one rank): 1 after the count scan, 2 after the
 # parent/insert/prefetch loads are issued, 3 after propagation, 4 after the hand-off check
+# (a build with -DSBMP_TL_PROLOGUE as well moves stamp 4 to the plan's barrier and stamp 5
+# to the located parent, splitting scan -> issued)
 STEP_NAMES = ["entry", "scan", "issued", "propagate", "handoff", "barrier", "end"]
 
 
