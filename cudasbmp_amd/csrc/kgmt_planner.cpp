@@ -938,7 +938,9 @@ void KgmtPlanner::run_to_goal() {
             continue;
         }
         if (t_next_ > p_.numIterations) break;   // every iteration launched: sync() ends it
-        if (hipStreamQuery(stream_) == hipSuccess && (int)((*w) >> 2) < issued) break;   // (no word came: sync() decides)
+        // the stream drained (or failed) without the word this loop waits for: sync() decides
+        const hipError_t q = hipStreamQuery(stream_);
+        if (q != hipErrorNotReady && (q != hipSuccess || (int)((*w) >> 2) < issued)) break;
         __builtin_ia32_pause();
     }
     sync();
