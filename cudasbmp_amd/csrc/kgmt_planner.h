@@ -198,7 +198,6 @@ private:
     };
     PollBuf* poll_ = nullptr;
     void run_to_goal();                   // run_plan() for a single k_step rank
-    std::vector<hipEvent_t> planEvents_;  // run_to_goal: one per iteration in flight (a ring)
     bool wallFixed_ = false;              // wallMs_ was taken at the goal iteration's end
     bool flushed_ = true;     // k_step mode: the last enqueued iteration has been inserted
     int lastFolded_ = 0;      // iterations <= lastFolded_ are in R2Valid / R2Invalid

@@ -1,7 +1,10 @@
+"""TTFS probe (GPU box): plan() on the reference demo, seeds 1..10, against enqueueing exactly the
+iterations each seed needs and one synchronisation.  python3 tools/ttfs_probe.py"""
 import time, numpy as np, sys, os
-sys.path.insert(0, os.getcwd())
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
 from cudasbmp_amd import KGMT, DeviceBuffer, read_obstacles_csv
-obs = read_obstacles_csv("configurations/obstacles/obstacles.csv")
+obs = read_obstacles_csv(os.path.join(ROOT, "configurations", "obstacles", "obstacles.csv"))
 d_obs = DeviceBuffer(obs)
 INIT = (5, 5, 0, 0, 0, 0, 0); GOAL = (2, 18, 0, 0, 0, 0, 0)
 k = KGMT(20.0, 20.0, 16, 8, 100, 30000, 10, 1.0, 0.5, agent="car")
