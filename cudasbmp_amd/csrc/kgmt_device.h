@@ -77,7 +77,7 @@ constexpr int kMaxRegObs = 8;
 constexpr int kMaxRanks = 8;         // ranks of one sharded planning problem (one node)
 constexpr int obs_in_registers(int obs) { return obs >= kObsReg ? obs - kObsReg : 0; }
 constexpr int kTimelineStamps = 8;   // s_memrealtime stamps per k_expand wave (diagnostics)
-constexpr int kFoldEvery = 64;       // iterations per R2 key-log fold (k_fold_r2 at c3: 19.9 us per 64, 15.4 per 32, ≈ 14 per 16)
+constexpr int kFoldEvery = 64;       // iterations per R2 key-log fold (k_fold_r2 at c3, round 5: 24.3-24.8 us per 64, 12.2-12.6 per 20)
 #ifndef SBMP_FOLD_KEYS
 #define SBMP_FOLD_KEYS 65280
 #endif
