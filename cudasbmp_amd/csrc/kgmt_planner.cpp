@@ -910,7 +910,10 @@ void KgmtPlanner::run_plan() {
 }
 
 void KgmtPlanner::run_to_goal() {
-    constexpr int kAhead = 3;   // iterations in flight (6 measured slower: 0.176-0.182 against 0.163 ms)
+#ifndef SBMP_PLAN_AHEAD
+#define SBMP_PLAN_AHEAD 3
+#endif
+    constexpr int kAhead = SBMP_PLAN_AHEAD;   // iterations in flight (2, 3, 4 within noise; 6 slower: profiles/r05/ttfs/)
     const volatile unsigned long long* w = &poll_->word;
     int issued = t_next_ - 1;   // iterations launched
     int goalSeen = -1;          // the launch whose planner first reported the goal (or the loop's end)
