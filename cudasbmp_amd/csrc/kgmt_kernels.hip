@@ -1237,6 +1237,76 @@ __global__ void k_mirror_check(MirrorProbe a, int pass) {
     }
     if (bad) atomicAdd(a.bad, bad);
 }
+// ------------------------------------------------------------------ fused-exchange check
+// The fused exchange's in-kernel order (k_step_exchange), reproduced once at start-up on
+// this machine (KgmtPlanner::fused_self_test): every workgroup pushes its
+// entries into every rank's list mirror with the system-scope stores k_step uses, drains
+// them (s_waitcnt vmcnt(0), barrier) and arrives with one relaxed agent-scope add on the
+// replicated, sharded counters; the workers (owned blocks 0..7) wait for every arrival,
+// fence (which orders only their own stores) and raise their flags at the peers, then
+// wait for the peers' flags; the next launch on each rank (k_mirror_check) reads its
+// mirror with plain loads.  No host barrier and no kernel boundary sits between a peer's
+// pushes and its flags: the order the fused exchange relies on, which the list-mirror
+// check (pushes in a launch of their own, then a host barrier) does not probe.
+__global__ __launch_bounds__(kBlock) void k_fx_probe(FxProbe a, int pass) {
+    const int tid = (int)threadIdx.x;
+    const int b = (int)blockIdx.x;              // owned block
+    const int g = a.rank + a.nranks * b;        // its global block
+    if (tid < 2 * a.entries) {   // entry (parity, g, i) in every rank's mirror, as k_step pushes
+        const int par = tid / a.entries, i = tid % a.entries;
+        const size_t o = ((size_t)par * a.nBlocks + g) * kBlock * kStepEntry + (size_t)i * kStepEntry;
+        for (int q = 0; q < a.nranks; ++q)
+            for (int k = 0; k < kStepEntry; ++k) store_record_g(G(a.peer[q]) + o + k, probe_entry(a.rank, g, i, k, pass));
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's pushes have completed
+    __syncthreads();
+    const int shard = b & (kFxShards - 1);
+    if (tid < kFxReplicas)   // the arrival: one instruction, lane r adding to replica r's shard counter
+        __hip_atomic_fetch_add(G(a.arrive) + (tid * kFxShards + shard) * kFxStride, 1u, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+    const int nW = min(kFxReplicas, a.owned);
+    if (b >= nW) return;
+    if (tid < kFxShards) {   // worker b: replica b's shard counters, until every workgroup is in
+        const SBMP_GAS unsigned* const rep = G(a.arrive) + (b * kFxShards + tid) * kFxStride;
+        const unsigned want = (unsigned)((a.owned - tid + kFxShards - 1) / kFxShards);
+        const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
+        while (true) {
+            const bool in = __hip_atomic_load(rep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= want;
+            if (__ballot(!in) == 0ull) break;
+            if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > kExchangeWaitTicks) {
+                if (tid == 0) atomicExch(a.error, kErrExchange);
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    __syncthreads();
+    if (a.nranks > 1) {
+        __threadfence_system();
+        __syncthreads();
+        if (tid < a.nranks && tid != a.rank) {   // flag (rank, chunk b) at peer q; wait for (q, chunk b) here
+            const int q = tid;
+            __hip_atomic_store(a.inbox[q] + a.flagsOff + (size_t)a.rank * kOneshotChunks + b, a.seq, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_SYSTEM);
+            unsigned long long* f = a.inbox[a.rank] + a.flagsOff + (size_t)q * kOneshotChunks + b;
+            const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
+            while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < a.seq) {
+                if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > kExchangeWaitTicks) {
+                    atomicExch(a.error, kErrExchange);
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(1);
+            }
+        }
+        __threadfence_system();
+        __syncthreads();
+    }
+}
+void launch_fx_probe(const FxProbe& a, int pass, hipStream_t s) {
+    hipLaunchKernelGGL(k_fx_probe, dim3(a.owned), dim3(kBlock), 0, s, a, pass);
+}
+
 void launch_mirror_probe(const MirrorProbe& a, int phase, int pass, float* sink, hipStream_t s) {
     const int n = 2 * a.blocks * a.entries;
     const dim3 grid((n + kBlock - 1) / kBlock), block(kBlock);
@@ -1579,6 +1649,9 @@ __device__ __forceinline__ void step_planner(const KgmtDev& d, const ShardView& 
                        : *reinterpret_cast<const SBMP_GAS int4*>(G(d.stepCnt) + (size_t)pp * kMaxStepBlocks + tid * 4);
     const IterCtrl pc = G(d.ctrl)[t - 1];
     const int goalIdx = G(d.status)->goalIdx;
+    // a bounded wait of an earlier launch gave up: the host's plan loop stops (hostPoll's
+    // "ended" bit) and raises it (KgmtPlanner::run_to_goal)
+    const int errPrev = G(d.status)->error;
     const SBMP_GAS int* tabPrev = G(d.R1) + (size_t)pp * 5 * d.nR1;
     int r1 = tabPrev[cell], r1a = tabPrev[d.nR1 + cell], r1v = tabPrev[2 * d.nR1 + cell],
         r1i = tabPrev[3 * d.nR1 + cell], r1c = tabPrev[4 * d.nR1 + cell];
@@ -1648,6 +1721,9 @@ __device__ __forceinline__ void step_planner(const KgmtDev& d, const ShardView& 
             c.run = 0;
             c.H = pc.H;
             st_ctrl(d.ctrl, t, c);
+            if (d.hostPoll)   // the loop has ended (goal, limit or tree full in t-1): say so as well
+                __hip_atomic_store(G(d.hostPoll), ((unsigned long long)t << 2) | 2ull | (goalIdx != kNoGoal ? 1ull : 0ull),
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         }
         return;
     }
@@ -1761,7 +1837,8 @@ __device__ __forceinline__ void step_planner(const KgmtDev& d, const ShardView& 
         if (q.newGoal != goalIdx) store_wt(reinterpret_cast<int*>(d.status), 0, q.newGoal);   // .goalIdx
         if (d.hostPoll)   // the host's plan loop: this launch planned t (a vector store over PCIe)
             __hip_atomic_store(G(d.hostPoll),
-                               ((unsigned long long)t << 2) | (q.runT ? 0ull : 2ull) | (q.newGoal != kNoGoal ? 1ull : 0ull),
+                               ((unsigned long long)t << 2) | (q.runT && !errPrev ? 0ull : 2ull) |
+                                   (q.newGoal != kNoGoal ? 1ull : 0ull),
                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
     // Insert t-1's flagged children (rows tsPrev + j, KGMT.cu:540-593) when they are

@@ -56,6 +56,20 @@ struct MirrorProbe {
     int* bad;
 };
 void launch_mirror_probe(const MirrorProbe& a, int phase, int pass, float* sink, hipStream_t s);
+// The fused exchange's order at start-up (KgmtPlanner::fused_self_test): `owned` workgroups
+// push entries (both parities, entries < entries, their global block) into every rank's
+// mirror, drain, arrive on the replicated sharded counters; the workers flag the peers and
+// wait for theirs.  k_mirror_check (phase 2 of launch_mirror_probe) reads the mirror next.
+struct FxProbe {
+    float4* peer[kMaxRanks];                 // every rank's mirror, mapped here
+    unsigned long long* inbox[kMaxRanks];    // every rank's one-shot inbox (flags at flagsOff)
+    size_t flagsOff;
+    int nranks, rank, nBlocks, owned, entries;
+    unsigned* arrive;                        // [kFxReplicas][kFxShards][kFxStride], zeroed per pass
+    unsigned long long seq;
+    int* error;
+};
+void launch_fx_probe(const FxProbe& a, int pass, hipStream_t s);
 // error: the planner's status word (set to kErrExchange when a peer never arrives).
 // compact (sharded k_step): the send layout, sent in compact form (kgmt_kernels.hip).
 struct OneshotLayout {

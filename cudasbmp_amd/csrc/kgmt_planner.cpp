@@ -400,6 +400,19 @@ KgmtPlanner::KgmtPlanner(const sbmp_kgmt_params& p, int nranks, int rank, Exchan
             d.xc = oneshot_compact(l);
             if (d.xc.total > (int)xWords_) d.fusedX = 0;   // cannot happen (compact is smaller)
         }
+        // The fused exchange orders a peer's mirror pushes before its flags inside one
+        // launch (drained stores, relaxed arrivals, the workers' fence and flags), with no
+        // kernel boundary between them: checked once here, on this machine; on failure
+        // every rank (the verdict is all-reduced) runs the exchange as its own k_oneshot,
+        // whose launch boundary follows the pushes (SBMP_FUSED_EXCHANGE=0's form).
+        if (d.fusedX) {
+            fusedCheck_ = fused_self_test() ? 1 : -1;
+            if (fusedCheck_ < 0) {
+                d.fusedX = 0;
+                fprintf(stderr, "sbmp: rank %d: the fused exchange failed its start-up check on this machine; "
+                                "the exchange runs as its own k_oneshot launch\n", rank);
+            }
+        }
     }
 }
 
@@ -482,6 +495,66 @@ bool KgmtPlanner::mirror_self_test() {
     bool ok = bad == 0;
     if (!ok) fprintf(stderr, "sbmp: rank %d: list mirror check: %d stale or wrong words\n", d_.rank, bad);
     if (const char* f = getenv("SBMP_MIRROR_SELFTEST"))   // tests: this rank reports a failure
+        if (std::string(f) == "fail") ok = false;
+    const unsigned long long badv = ok ? 0ull : 1ull;
+    SBMP_HIP(hipMemcpyAsync(verdict, &badv, sizeof(badv), hipMemcpyHostToDevice, stream_));
+    ex_->allreduce_u64(verdict, verdict + 1, 1, stream_);
+    unsigned long long anyBad = 0;
+    SBMP_HIP(hipMemcpyAsync(&anyBad, verdict + 1, sizeof(anyBad), hipMemcpyDeviceToHost, stream_));
+    SBMP_HIP(hipStreamSynchronize(stream_));
+    return anyBad == 0;
+}
+
+// The fused exchange's in-kernel order checked once on this machine (k_fx_probe,
+// kgmt_kernels.hip): per pass, every rank's plain loads cache the probed
+// mirror lines (k_mirror_touch), a host barrier, then one launch in which every owned
+// workgroup pushes its entries into every rank's mirror, drains, arrives, and the workers
+// exchange flags with the peers, then a new launch reads the mirror with plain loads
+// (k_mirror_check).  Probed: both parities, the first 64 entries of every global block,
+// two passes (patterns 2 and 3: the list-mirror check used 0 and 1).  The verdicts and
+// any timed-out wait are all-reduced.  SBMP_FUSED_SELFTEST=fail: this rank reports a
+// failure (tests).
+bool KgmtPlanner::fused_self_test() {
+    const int P = d_.nranks;
+    MirrorProbe m{};
+    FxProbe a{};
+    for (int q = 0; q < P; ++q) {
+        m.peer[q] = a.peer[q] = d_.mirrorPeer[q];
+        a.inbox[q] = d_.xInbox[q];
+    }
+    m.own = d_.stepMirror;
+    m.nranks = a.nranks = P;
+    m.rank = a.rank = d_.rank;
+    m.nBlocks = a.nBlocks = d_.nBlocks;
+    m.blocks = d_.nBlocks;
+    m.entries = a.entries = 64;
+    a.owned = expandBlocks_;
+    a.flagsOff = (size_t)2 * P * xWords_;
+    a.arrive = alloc<unsigned>((size_t)kFxCounters * kFxStride);
+    a.error = &d_.status->error;
+    int* dev = alloc<int>(2);   // [bad, sink]
+    m.bad = dev;
+    unsigned long long* verdict = alloc<unsigned long long>(2);
+    SBMP_HIP(hipMemsetAsync(dev, 0, sizeof(int) * 2, stream_));
+    SBMP_HIP(hipMemsetAsync(&d_.status->error, 0, sizeof(int), stream_));
+    for (int pass = 2; pass < 4; ++pass) {
+        launch_mirror_probe(m, 0, pass, reinterpret_cast<float*>(dev + 1), stream_);   // old lines cached
+        SBMP_HIP(hipMemsetAsync(a.arrive, 0, sizeof(unsigned) * kFxCounters * kFxStride, stream_));
+        ex_->barrier(stream_);   // every rank's touch before any push
+        a.seq = ++xSeq_;         // the same count on every rank (the fused exchange's base follows it)
+        launch_fx_probe(a, pass, stream_);
+        launch_mirror_probe(m, 2, pass, nullptr, stream_);   // the next launch: plain loads, compared
+    }
+    SBMP_HIP(hipGetLastError());
+    int bad = 0, error = 0;
+    SBMP_HIP(hipMemcpyAsync(&bad, dev, sizeof(int), hipMemcpyDeviceToHost, stream_));
+    SBMP_HIP(hipMemcpyAsync(&error, &d_.status->error, sizeof(int), hipMemcpyDeviceToHost, stream_));
+    SBMP_HIP(hipStreamSynchronize(stream_));
+    SBMP_HIP(hipMemsetAsync(&d_.status->error, 0, sizeof(int), stream_));
+    bool ok = bad == 0 && error == 0;
+    if (!ok) fprintf(stderr, "sbmp: rank %d: fused exchange check: %d stale or wrong words, wait error %d\n", d_.rank,
+                     bad, error);
+    if (const char* f = getenv("SBMP_FUSED_SELFTEST"))   // tests: this rank reports a failure
         if (std::string(f) == "fail") ok = false;
     const unsigned long long badv = ok ? 0ull : 1ull;
     SBMP_HIP(hipMemcpyAsync(verdict, &badv, sizeof(badv), hipMemcpyHostToDevice, stream_));
@@ -588,6 +661,13 @@ void KgmtPlanner::begin(const float* initial, const float* goal, const float* d_
     // curand_init(seed, slot, 0) for every slot (KGMT.cu:109-111, D1).
     launch_init_slots(d, curand_seed_state(seed), jumps_, nbits_, expandBlocks_, s);
     SBMP_HIP(hipGetLastError());
+    // tests: SBMP_INJECT_WAIT_ERROR=<kErr*> starts the plan as if a bounded in-kernel wait
+    // had already given up, so the host's error paths can be exercised without a hang
+    if (const char* inj = getenv("SBMP_INJECT_WAIT_ERROR")) {
+        const int code = atoi(inj);
+        SBMP_HIP(hipStreamSynchronize(s));   // after k_seed_root's reset
+        SBMP_HIP(hipMemcpy(&d.status->error, &code, sizeof(int), hipMemcpyHostToDevice));
+    }
 
     t_next_ = 1;
     lastFolded_ = 0;
@@ -663,6 +743,7 @@ void KgmtPlanner::path_info(sbmp_path_info* out) {
     out->fusedExchange = d.fusedX ? 1 : 0;
     out->oneshotCheck = oneshotCheck_;
     out->mirrorCheck = mirrorCheck_;
+    out->fusedCheck = fusedCheck_;
 }
 
 void KgmtPlanner::build_grid(const float* d_obstacles, int nObs) {
@@ -899,9 +980,11 @@ void Planner::run(int pollEvery) {
 // synchronisations (run(8): a flush launch, two copies and a synchronisation every 8
 // iterations).  The planner of launch t inserts t-1's children and checks them for the
 // goal, so when its word says "goal" (or "loop ended"), the plan ends with launch t:
-// wallMs is taken when launch t has ended (the next launch's planner has stored its word,
-// or the stream is idle), before the launches already queued behind it (no-ops: a found
-// goal or an ended loop stops every later iteration) drain.
+// wallMs is taken when launch t has ended (the next launch's planner has stored its word:
+// a planner whose loop has ended stores it too; or the stream is idle), before the
+// launches already queued behind it (no-ops: a found goal or an ended loop stops every
+// later iteration) drain.  A planner that finds status.error set (an earlier launch's
+// bounded wait gave up) reports the loop as ended, and the error is raised after sync().
 // Time-to-first-solution is then the end of the iteration that inserts the goal node
 // (BASELINE.md), without the polls.  The result is the same as run(8)'s.
 void KgmtPlanner::run_plan() {
@@ -943,6 +1026,11 @@ void KgmtPlanner::run_to_goal() {
         __builtin_ia32_pause();
     }
     sync();
+    // a bounded in-kernel wait that gave up (its planner's word ended the loop above):
+    // raised here, as run(8) raises it from active(), whether or not a result is read
+    SBMP_HIP(hipMemcpyAsync(&poll_->status, d_.status, sizeof(PlannerStatus), hipMemcpyDeviceToHost, stream_));
+    SBMP_HIP(hipStreamSynchronize(stream_));
+    if (poll_->status.error) throw_wait_error(poll_->status.error);
 }
 
 void KgmtPlanner::result(sbmp_plan_result* r) {

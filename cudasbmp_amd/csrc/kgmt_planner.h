@@ -216,7 +216,8 @@ private:
     bool oneshot_ = false;                   // sharded: the exchange is k_oneshot over IPC-mapped inboxes
     bool oneshot_self_test();                // k_oneshot checked once at construction (all ranks agree)
     bool mirror_self_test();                 // the list mirror checked once at construction (all ranks agree)
-    int oneshotCheck_ = 0, mirrorCheck_ = 0;   // start-up checks: 0 not run, 1 passed, -1 failed (fell back)
+    bool fused_self_test();                  // the fused exchange's in-kernel order, likewise
+    int oneshotCheck_ = 0, mirrorCheck_ = 0, fusedCheck_ = 0;   // start-up checks: 0 not run, 1 passed, -1 failed (fell back)
     unsigned long long* inbox_[kMaxRanks] = {nullptr};
     bool compactX_ = true;   // sharded k_step: k_oneshot sends the compact form of the exchange
     unsigned long long xSeq_ = 0;            // exchanges so far (the same count on every rank)

@@ -121,6 +121,10 @@ typedef struct sbmp_path_info {
     int mirrorCheck;          /* start-up check of the list mirror (stores into peers' mirrors
                                  seen after a kernel boundary): 0 not run, 1 passed, -1 failed
                                  on some rank (every rank then reads the lists over the mapping) */
+    int fusedCheck;           /* start-up check of the fused exchange's in-kernel order (pushes
+                                 drained, relaxed arrivals, the workers' flags, the peers' next
+                                 launch reading the mirror): 0 not run, 1 passed, -1 failed on some
+                                 rank (every rank then runs the exchange as its own k_oneshot) */
 } sbmp_path_info;
 
 typedef struct sbmp_kgmt sbmp_kgmt;

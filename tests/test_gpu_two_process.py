@@ -61,6 +61,10 @@ def _rank_main(rank, port, kw, seed, out_dir, exchange, delay=0.0):
         os.environ["SBMP_MIRROR_SELFTEST"] = "fail"
     else:
         os.environ.pop("SBMP_MIRROR_SELFTEST", None)
+    if exchange == "fused-check-fails" and rank == 1:   # only rank 1's fused-exchange check "fails"
+        os.environ["SBMP_FUSED_SELFTEST"] = "fail"
+    else:
+        os.environ.pop("SBMP_FUSED_SELFTEST", None)
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     import torch.distributed as dist
@@ -80,7 +84,7 @@ def _rank_main(rank, port, kw, seed, out_dir, exchange, delay=0.0):
     oneshots = g.kernel_stats().get("k_oneshot", (0, 0.0))[0]
     pinfo = g.path_info()
     mirror, fused = pinfo["list_mirror"], pinfo["fused_exchange"]
-    checks = np.array([pinfo["oneshot_check"], pinfo["mirror_check"]])
+    checks = np.array([pinfo["oneshot_check"], pinfo["mirror_check"], pinfo["fused_check"]])
     digest = np.uint64(g.state_hash())   # the replicated state: the same on both ranks
     s, p, c = g.tree()
     G, GN = g.flags()          # GNew words live with their owner: merged by the all-reduce
@@ -119,6 +123,10 @@ def _rank_main(rank, port, kw, seed, out_dir, exchange, delay=0.0):
     # it the fused exchange) together and read the lists over the mapping with k_oneshot
     (dict(samplesPerIteration=4096, batchRule="fill", maxTreeSize=200000, numIterations=15, goalThreshold=0.0), 21,
      "mirror-check-fails", 0.0),
+    # rank 1's start-up check of the fused exchange's in-kernel order fails: both ranks keep
+    # the mirror and run the exchange as its own k_oneshot launch, together
+    (dict(samplesPerIteration=4096, batchRule="fill", maxTreeSize=200000, numIterations=15, goalThreshold=0.0), 21,
+     "fused-check-fails", 0.0),
 ])
 def test_two_processes_one_gpu_bit_exact(kw, seed, exchange, delay, tmp_path, obstacles, oracle_lib):
     ctx = mp.get_context("spawn")
@@ -154,16 +162,18 @@ def test_two_processes_one_gpu_bit_exact(kw, seed, exchange, delay, tmp_path, ob
         # lists over the mapping, with k_oneshot; the collective exchange uses neither
         fused = exchange == "oneshot"
         assert bool(d["fused"]) == fused, f"rank {r}: fused exchange {bool(d['fused'])}"
-        assert bool(d["mirror"]) == (exchange in ("oneshot", "oneshot-kernel")), \
+        assert bool(d["mirror"]) == (exchange in ("oneshot", "oneshot-kernel", "fused-check-fails")), \
             f"rank {r}: list mirror {bool(d['mirror'])}"
-        if exchange in ("oneshot-kernel", "oneshot-remote", "mirror-check-fails"):
+        if exchange in ("oneshot-kernel", "oneshot-remote", "mirror-check-fails", "fused-check-fails"):
             assert int(d["oneshots"]) > 0, f"rank {r}: the one-shot exchange did not run"
         else:
             assert int(d["oneshots"]) == 0, f"rank {r}: k_oneshot ran ({int(d['oneshots'])} launches)"
         # the start-up checks: which ran, and the all-reduced verdict every rank acted on
-        want = {"collective": ["not run", "not run"], "oneshot-check-fails": ["failed", "not run"],
-                "oneshot-remote": ["passed", "not run"], "mirror-check-fails": ["passed", "failed"]}.get(
-                    exchange, ["passed", "passed"])
+        want = {"collective": ["not run"] * 3, "oneshot-check-fails": ["failed", "not run", "not run"],
+                "oneshot-remote": ["passed", "not run", "not run"],
+                "mirror-check-fails": ["passed", "failed", "not run"],
+                "oneshot-kernel": ["passed", "passed", "not run"],
+                "fused-check-fails": ["passed", "passed", "failed"]}.get(exchange, ["passed"] * 3)
         assert d["checks"].tolist() == want, f"rank {r}: start-up checks {d['checks'].tolist()}"
     assert len({int(d["digest"]) for d in R}) == 1, "the ranks' replicated states differ"
     for r, d in enumerate(R):   # every rank holds the whole tree and the merged exports
