@@ -90,7 +90,7 @@ class InsertBatchArgs(ctypes.Structure):   # sbmp_insert_batch_args
 class PathInfo(ctypes.Structure):   # sbmp_path_info
     _fields_ = [(n, ctypes.c_int) for n in ("stepForm", "obstacleForm", "residentGroups", "neededGroups", "exchange",
                                             "nranks", "rank", "commRanks", "listMirror",
-                                            "fusedExchange", "oneshotCheck", "mirrorCheck", "fusedCheck")]
+                                            "fusedExchange", "oneshotCheck", "mirrorCheck", "fusedCheck", "rowTableLds")]
 
 
 class KernelStat(ctypes.Structure):

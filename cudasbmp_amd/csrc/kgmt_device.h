@@ -234,6 +234,8 @@ struct KgmtDev {
     int listPlain;   // sharded lists readable with plain loads (the mirror, or a local shard group)
     int xRowOff, xCntOff, xNewOff;   // u64 offsets of the row words, block words and R2New bytes
     int xC16Off;   // u64 offset of the block counts as u16 (global block order; 16-B aligned): k_step's LDS row table
+    int c16Lds;    // sharded k_step stages that table in LDS (else: a row's block words from the exchange, one
+                   // more L2 round trip per lookup; chosen by begin() when the table would cost residency)
     // k_step reads this struct from device memory (a copy the host refreshes before a
     // launch when it changed): as a 600-B kernel argument its fields were loaded at
     // entry, spilled to VGPR lanes and reloaded, four serial scalar round trips
@@ -568,13 +570,25 @@ __device__ __forceinline__ void sincos_pred(float x, float* s, float* c) {
 // (-pi, pi], so reduce_pio2 always takes its Cody-Waite branch and the argument is
 // finite: the non-finite and Payne-Hanek paths of tanf_d are dead here, and the
 // result is bitwise tanf_d's (same operations on the same reduced value).
+// The odd quadrants' -1/t as v_rcp_f32 and one Newton step instead of the IEEE division
+// (3 VALU instead of ~11): the same bits for every t this function can see.  An odd
+// quadrant means |x| in [pi/4, 3pi/4], where |r| >= |float(pi/2) - pi/2| = 4.4e-8 and
+// |t| <= 1, far from the range ends where the Newton form loses correct rounding;
+// tools/microbench/tan_rcp_check.hip compares both forms on every float in [-pi, pi]
+// (profiles/r06/tan_rcp_check.txt: no mismatch).  -DSBMP_TAN_IEEE keeps the division.
 __device__ __forceinline__ float tan_steer(float x) {
     const float j = __builtin_rintf(x * 0.636619772f);
     float r = __builtin_fmaf(j, -1.57079601e+00f, x);
     r = __builtin_fmaf(j, -3.13916473e-07f, r);
     r = __builtin_fmaf(j, -5.39030253e-15f, r);
     const float t = tan_poly(r);
+#ifdef SBMP_TAN_IEEE
     return ((int)j & 1) ? -1.0f / t : t;
+#else
+    const float y = __builtin_amdgcn_rcpf(t);
+    const float e = __builtin_fmaf(-t, y, 1.0f);
+    return ((int)j & 1) ? -__builtin_fmaf(e, y, y) : t;
+#endif
 }
 
 // Wave-level culling of the per-step tests (register obstacle lists).  Every
@@ -1019,7 +1033,10 @@ __device__ __forceinline__ StepSched car_schedule(float4 p, int parent, bool act
     return s;
 }
 
-template <int OBS, bool PH>
+// UNIT_L: agentLength == 1 (invAgentLength == 1, the reference demo's and every bench
+// workload's): v / L is v itself (finite states, D15), so the heading rate is one multiply,
+// v tan(steering), with the same bits as (v * 1) tan(steering).
+template <int OBS, bool PH, bool UNIT_L = false>
 __device__ __forceinline__ bool car_euler_fast(float4 p, const ChildCtl& ctl, const KgmtDev& d, const float4* obs,
                                                const WaveCull& cull, const StepSched& sched, ChildOut& out) {
     constexpr int NOBS = obs_in_registers(OBS);
@@ -1047,7 +1064,7 @@ __device__ __forceinline__ bool car_euler_fast(float4 p, const ChildCtl& ctl, co
         else sincos_cw(vt.y, &st, &ct);
         const sbmp_f32x2 nxy = __builtin_elementwise_fma(sbmp_f32x2{vt.x, vt.x} * sbmp_f32x2{ct, st}, dt2, xy);
         const sbmp_f32x2 far = wh - nxy;   // W - x, H - y
-        const float vl = vt.x * invL;     // v / L, exact for a power-of-two L
+        const float vl = UNIT_L ? vt.x : vt.x * invL;     // v / L, exact for a power-of-two L
         const sbmp_f32x2 nvt = __builtin_elementwise_fma(sbmp_f32x2{a, vl * ctl.tanS}, dt2, vt);
         float sep = 1.0f;   // >= 0: free of every kept box
         if (keptNow) {

@@ -1508,8 +1508,22 @@ __device__ __forceinline__ void row_locate_lds(const ShardView& sv, const uint16
     *block = r * sv.nranks + q;
     *idx = off;
 }
+// A position inside row r: from the LDS table when the launch staged it (d.c16Lds, the
+// default), else from the row's block words (one dependent L2 round trip, round 4's form;
+// begin() picks it when the table's LDS would leave too few workgroups resident).
+__device__ __forceinline__ void row_locate_any(const KgmtDev& d, const ShardView& sv, const uint16_t* sC16, int r,
+                                               int off, int* block, int* idx) {
+    if (d.c16Lds) {   // uniform
+        row_locate_lds(sv, sC16, r, off, block, idx);
+    } else {
+        int w[kMaxRanks];
+        row_words(sv, r, w);
+        row_locate(sv, w, r, off, block, idx);
+    }
+}
 // Sharded prologue: the exchange's u16 block counts (nBlocks of them, 16-B padded) into
-// LDS, loaded with the first batch (issue) and stored once the scan has waited for it.
+// LDS, loaded with the first batch (issue) and stored once the scan has waited for it
+// (none when d.c16Lds is 0: the exact-size buffer is then empty).
 struct C16Load {
     uint4 v[kMaxRanks / 2];   // 1,024 rows x P u16 over 256 threads: at most 4 x 16 B each
 };
@@ -1517,7 +1531,7 @@ __device__ __forceinline__ C16Load c16_issue(const KgmtDev& d) {
     C16Load c;
     // an exact-size buffer: loads past the table return 0 without a memory access, so every
     // load is issued unconditionally (no branch, one batch)
-    const int n16 = (d.nBlocks + 7) >> 3;
+    const int n16 = d.c16Lds ? (d.nBlocks + 7) >> 3 : 0;
     const __amdgpu_buffer_rsrc_t r =
         __builtin_amdgcn_make_buffer_rsrc(const_cast<unsigned long long*>(d.stepXr + d.xC16Off), (short)0, n16 * 16,
                                           kBufferDword3);
@@ -1529,7 +1543,7 @@ __device__ __forceinline__ C16Load c16_issue(const KgmtDev& d) {
     return c;
 }
 __device__ __forceinline__ void c16_store(const KgmtDev& d, const C16Load& c, uint16_t* sC16) {
-    const int n16 = (d.nBlocks + 7) >> 3;
+    const int n16 = d.c16Lds ? (d.nBlocks + 7) >> 3 : 0;
 #pragma unroll
     for (int u = 0; u < kMaxRanks / 2; ++u) {
         const int i = (int)threadIdx.x + u * kBlock;
@@ -1854,7 +1868,7 @@ __device__ __forceinline__ void step_planner(const KgmtDev& d, const ShardView& 
                 if (lo + step < nS && sPfx[lo + step] <= j) lo += step;
             if constexpr (SH) {
                 int blk, idx;
-                row_locate_lds(sv, sC16, lo, j - sPfx[lo], &blk, &idx);
+                row_locate_any(d, sv, sC16, lo, j - sPfx[lo], &blk, &idx);
                 return list_entry<SH>(d, pp, blk, idx);
             } else {
                 return list_entry<SH>(d, pp, lo, j - sPfx[lo]);
@@ -2095,7 +2109,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) voi
                     const int j = j0 + o, dst = q.tsPrev + j;
                     if (j < q.nIns && dst < d.M) {   // D13: the reference writes past M here
                         int blk, idx;
-                        row_locate_lds(sv, sC16, b, o, &blk, &idx);
+                        row_locate_any(d, sv, sC16, b, o, &blk, &idx);
                         const SBMP_GAS float4* e = list_entry<SH>(d, pp, blk, idx);
                         const float4 s4 = list_load<SH>(d, e);
                         const float4 u4 = list_load<SH>(d, e + 1);
@@ -2169,7 +2183,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) voi
         if (fromList) {
             if constexpr (SH) {   // the row's blocks: from the LDS table (round 4: one more L2 round trip)
                 int blk, idx;
-                row_locate_lds(sv, sC16, lo, j - sPfx[lo], &blk, &idx);
+                row_locate_any(d, sv, sC16, lo, j - sPfx[lo], &blk, &idx);
                 src = list_entry<SH>(d, pp, blk, idx);
             } else {
                 src = list_entry<SH>(d, pp, lo, j - sPfx[lo]);
@@ -2201,7 +2215,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) voi
     }
     // the grid index's cell-start table into LDS: every row lookup of the Euler loop is
     // then an LDS read instead of an L2 round trip (the boxes stay in global memory)
-    int* const sGridStart = SH ? reinterpret_cast<int*>(sC16 + ((d.nBlocks + 7) & ~7)) : reinterpret_cast<int*>(sNew + nW);
+    int* const sGridStart =
+        SH ? reinterpret_cast<int*>(sC16 + (d.c16Lds ? ((d.nBlocks + 7) & ~7) : 0)) : reinterpret_cast<int*>(sNew + nW);
     if constexpr (OBS == kObsGrid) {
         const int nStart = d.gridG * d.gridG + 1;
         const SBMP_GAS int* const gs = G(d.gridStart);
@@ -2230,10 +2245,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) voi
             const StepSched sched = car_schedule<OBS>(p, parent, act, d, oLane);
             WaveCull cull{~0u, true};   // the schedule covers the whole reach
             if (!sched.valid) cull = car_cull<OBS>(p, ctl, d, obs);
-            if (__ballot(!car_theta_bounded(p, ctl, d)) == 0ull)
-                valid = car_euler_fast<OBS, false>(p, ctl, d, obs, cull, sched, out) && act;
-            else
+            if (__ballot(!car_theta_bounded(p, ctl, d)) != 0ull)   // rare: Payne-Hanek per lane
                 valid = car_euler_fast<OBS, true>(p, ctl, d, obs, cull, sched, out) && act;
+            else if (d.invAgentLength == 1.0f)   // per plan (uniform): L = 1, one multiply less per step
+                valid = car_euler_fast<OBS, false, true>(p, ctl, d, obs, cull, sched, out) && act;
+            else
+                valid = car_euler_fast<OBS, false>(p, ctl, d, obs, cull, sched, out) && act;
         }
     }
     if (!fast) {
@@ -2660,7 +2677,7 @@ void launch_expand(const KgmtDev& d, int t, int agent, int blocks, int variant, 
 static size_t step_lds_bytes(const KgmtDev& d, bool sh) {
     const size_t nS = sh ? d.nBlocks / d.nranks : d.nBlocks;   // scan entries: blocks, or rows
     size_t b = sizeof(int) * (nS + 1) + sizeof(uint32_t) * (size_t)(d.nR2 / 32);
-    if (sh) b = ((b + 15) & ~(size_t)15) + sizeof(uint16_t) * (((size_t)d.nBlocks + 7) & ~(size_t)7);
+    if (sh) b = ((b + 15) & ~(size_t)15) + (d.c16Lds ? sizeof(uint16_t) * (((size_t)d.nBlocks + 7) & ~(size_t)7) : 0);
     return b;
 }
 

@@ -692,6 +692,10 @@ void KgmtPlanner::choose_form(const float* d_obstacles, int nObs) {
     // layout is k_step's); both are bit-exact for every list.
     d.stepMode = stepCapable_ ? 1 : 0;
     neededGroups_ = 1 + (d.sharded ? d.nBlocks / d.nranks : d.nBlocks);
+    // a sharded rank stages the exchange's u16 block counts in LDS (2 B per global block)
+    // unless that costs residency (below) or SBMP_C16_LDS=0
+    const char* cv = getenv("SBMP_C16_LDS");
+    d.c16Lds = (d.sharded && !(cv && atoi(cv) == 0)) ? 1 : 0;
     StepResidency why;
     residentGroups_ = stepCapable_ ? step_resident_groups(d, p_.agent, expandVariant_, &why) : 0;
     // SBMP_STEP_RESIDENCY=warn: sharded ranks that share one GPU (a rehearsal on one
@@ -706,11 +710,24 @@ void KgmtPlanner::choose_form(const float* d_obstacles, int nObs) {
         formLogged_ = true;
     } else if (stepCapable_ && residentGroups_ < neededGroups_) {
         const int before = residentGroups_;
+        const char* how = "two launches per iteration";
+        auto fits = [&]() {
+            residentGroups_ = step_resident_groups(d, p_.agent, expandVariant_, &why);
+            return residentGroups_ >= neededGroups_;
+        };
         if (!d.sharded) {
             d.stepMode = 0;
+        } else if (d.c16Lds && (d.c16Lds = 0, fits())) {   // row positions from the block words instead
+            how = "this rank reads row positions from the exchange's block words (no LDS row table)";
         } else if (!d.gridStart && nObs > 0) {
             build_grid(d_obstacles, nObs);
-            residentGroups_ = step_resident_groups(d, p_.agent, expandVariant_, &why);
+            how = "this rank indexes the obstacles with the uniform grid";
+            d.c16Lds = (cv && atoi(cv) == 0) ? 0 : 1;
+            if (!fits() && d.c16Lds) {
+                d.c16Lds = 0;
+                (void)fits();
+                how = "this rank indexes the obstacles with the uniform grid, without the LDS row table";
+            }
         }
         if (d.sharded && residentGroups_ < neededGroups_)
             throw Error(SBMP_ERR_INVALID_ARGUMENT,
@@ -719,8 +736,7 @@ void KgmtPlanner::choose_form(const float* d_obstacles, int nObs) {
                             std::to_string(why.cus) + " CUs at " + std::to_string(why.dynLds) + " B of dynamic LDS)");
         if (!formLogged_) {
             fprintf(stderr, "sbmp: %d obstacles: k_step needs %d workgroups resident, the device holds %d; %s\n", nObs,
-                    neededGroups_, before,
-                    d.sharded ? "this rank indexes the obstacles with the uniform grid" : "two launches per iteration");
+                    neededGroups_, before, how);
             formLogged_ = true;
         }
     }
@@ -744,6 +760,7 @@ void KgmtPlanner::path_info(sbmp_path_info* out) {
     out->oneshotCheck = oneshotCheck_;
     out->mirrorCheck = mirrorCheck_;
     out->fusedCheck = fusedCheck_;
+    out->rowTableLds = d.c16Lds;
 }
 
 void KgmtPlanner::build_grid(const float* d_obstacles, int nObs) {

@@ -336,7 +336,8 @@ class KGMT:
                 "list_mirror": bool(pi.listMirror), "fused_exchange": bool(pi.fusedExchange),
                 "oneshot_check": {0: "not run", 1: "passed", -1: "failed"}.get(pi.oneshotCheck, pi.oneshotCheck),
                 "mirror_check": {0: "not run", 1: "passed", -1: "failed"}.get(pi.mirrorCheck, pi.mirrorCheck),
-                "fused_check": {0: "not run", 1: "passed", -1: "failed"}.get(pi.fusedCheck, pi.fusedCheck)}
+                "fused_check": {0: "not run", 1: "passed", -1: "failed"}.get(pi.fusedCheck, pi.fusedCheck),
+                "row_table_lds": bool(pi.rowTableLds)}
 
     def kernel_samples(self, name: str) -> np.ndarray:
         """Per-launch durations (ms) of kernel `name` since the last reset_kernel_stats()."""

@@ -125,6 +125,9 @@ typedef struct sbmp_path_info {
                                  drained, relaxed arrivals, the workers' flags, the peers' next
                                  launch reading the mirror): 0 not run, 1 passed, -1 failed on some
                                  rank (every rank then runs the exchange as its own k_oneshot) */
+    int rowTableLds;          /* sharded k_step: 1 stages the exchange's u16 block counts in LDS
+                                 (row positions without a dependent load); 0 reads a row's block
+                                 words (chosen when the table's LDS would cost residency) */
 } sbmp_path_info;
 
 typedef struct sbmp_kgmt sbmp_kgmt;

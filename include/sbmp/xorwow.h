@@ -47,9 +47,12 @@ SBMP_HD Xorwow xorwow_seed(uint64_t seed) {
     return st;
 }
 
-// curand_uniform: x * 2^-32 + 2^-33 (product exact, one rounding), in (0, 1].
+// curand_uniform: x * 2^-32 + 2^-33 (product exact, one rounding), in (0, 1].  Written as
+// one fused multiply-add: the product of the converted integer and a power of two is
+// exact, so the FMA rounds the same sum once, as the multiply-then-add does (one VALU per
+// draw instead of two; the oracle's restatement keeps the two operations, same bits).
 SBMP_HD float xorwow_uniform(Xorwow& s) {
-    return (float)xorwow_next(s) * 2.3283064365386963e-10f + 1.1641532182693481e-10f;
+    return __builtin_fmaf((float)xorwow_next(s), 2.3283064365386963e-10f, 1.1641532182693481e-10f);
 }
 
 }  // namespace sbmp

@@ -168,5 +168,35 @@ def test_c5_sharded_per_rank_shape_bit_exact(P, oracle_lib):
     info = g.path_info()
     assert info["form"] == "k_step" and info["obstacle_form"] == "grid" and info["nranks"] == P, info
     assert info["needed_groups"] == 1 + 512 and info["resident_groups"] >= info["needed_groups"], info
+    assert info["row_table_lds"], info
     assert r.iterations == 6 and g.iter_log()[:, 5].max() == 131072 * P
     assert_same_state(g, o, label=f"c5 per-rank shape, {P} ranks")
+
+
+def test_c5_sharded_1024_rows_without_row_table(oracle_lib):
+    """8 sharded ranks of 262,144 children (1,024 rows each) on the 10,000-box field: the
+    grid's cell-start table (20 KB) and the u16 row table of 8,192 blocks (16 KB) in LDS
+    leave three workgroups per CU (768 of the 1,025 k_step needs; ADVICE r05: begin()
+    refused this shape in round 5), so begin() drops the row table (row positions from the
+    exchange's block words, one more L2 round trip) and keeps k_step on the grid.  A local
+    group of 8 ranks on one GPU, 3 iterations, whole state bit-exact."""
+    obs = _c5_obstacles()
+    g, o, r = _run(_bench_kw(262144 * 8, 3, maxTreeSize=1 << 25), BENCH_SEED, obs, P=8)
+    info = g.path_info()
+    assert info["form"] == "k_step" and info["obstacle_form"] == "grid" and info["nranks"] == 8, info
+    assert info["needed_groups"] == 1 + 1024 and info["resident_groups"] >= info["needed_groups"], info
+    assert not info["row_table_lds"], info
+    assert r.iterations == 3 and g.iter_log()[:, 5].max() == 262144 * 8
+    assert_same_state(g, o, label="c5 1,024 rows per rank, no row table")
+
+
+@pytest.mark.parametrize("P", [2, 8])
+def test_sharded_row_table_off_bit_exact(P, obstacles, oracle_lib, monkeypatch):
+    """SBMP_C16_LDS=0 forces the block-word form of row positions on the c3 workload:
+    every lookup (parents from t-1's lists, the expanders' own-row inserts, the planner's
+    inserts) reads the row's block words; whole state bit-exact."""
+    monkeypatch.setenv("SBMP_C16_LDS", "0")
+    g, o, r = _run(_bench_kw(16384 * P, 12, maxTreeSize=1 << 22), BENCH_SEED, obstacles, P=P)
+    info = g.path_info()
+    assert info["form"] == "k_step" and not info["row_table_lds"], info
+    assert_same_state(g, o, label=f"row table off, {P} ranks")
