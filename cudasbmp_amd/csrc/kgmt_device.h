@@ -1018,8 +1018,11 @@ __device__ __forceinline__ StepSched car_schedule(float4 p, int parent, bool act
     const int i = (L < nb) ? L / (NOBS > 0 ? NOBS : 1) : L - nb;   // this lane's step
     const float t = (float)(i + 1) * d.reachStep;
     const float r = __builtin_fmaf(__builtin_fmaf(t, v, 2.5f * t * t), 1.0001f, 1e-3f);
-    // box item: L-inf distance of the lane's box from the parents' bounding box
-    const float db = __builtin_fmaxf(__builtin_fmaxf(oLane.x - xhi, xlo - oLane.z), __builtin_fmaxf(oLane.y - yhi, ylo - oLane.w));
+    // box item: L-inf distance of the lane's box from the parents' bounding box (the four
+    // differences as two packed subtractions, as in box_sep)
+    const sbmp_f32x2 dlo = sbmp_f32x2{oLane.x, oLane.y} - sbmp_f32x2{xhi, yhi};
+    const sbmp_f32x2 dhi = sbmp_f32x2{xlo, ylo} - sbmp_f32x2{oLane.z, oLane.w};
+    const float db = __builtin_fmaxf(vmax3(dlo.x, dlo.y, dhi.x), dhi.y);
     // workspace item: the box's distance to the workspace's edges (uniform)
     const float dw = __builtin_fminf(__builtin_fminf(xlo, ylo), __builtin_fminf(d.width - xhi, d.height - yhi));
     const bool isBox = L < nb;   // bitwise, no branch: both items are computed on every lane

@@ -215,14 +215,38 @@ __global__ __launch_bounds__(kBlock) void k_expand(KgmtDev d, int t) {
 
     bool accept = false;
     float4 cs = make_float4(0.f, 0.f, 0.f, 0.f), cc = cs;   // this slot's child (state, ctrl): the packed record
+    // Register lists, car: k_step's fast loop (round 6; the per-step box schedule, the
+    // separation-metric box tests, Cody-Waite alone where theta stays in range,
+    // DESIGN.md §5.5), on every lane outside any divergent branch: lanes past S propagate
+    // row 0 with the zero state the exact-size buffer gave them, and their result is
+    // dropped (nothing of theirs is stored).  Other forms: the exec-masked car_euler.
+    Xorwow rs{ra.x, ra.y, ra.z, ra.w, rb.x, rb.y};
+    ChildOut out;
+    bool valid = false, fast = false;
+    if constexpr (AGENT == 0 && kRegObs > 0) {
+        fast = car_fast_ok(d);   // per plan (uniform)
+        if (fast) {
+            const ChildCtl ctl = draw_controls<0>(rs, d);
+            // box (lane % n) for the schedule: a load of its own (indexing ro[] by lane would put
+            // the register list in scratch)
+            const float4 oLane = G(d.obstacles)[lane % kRegObs];
+            const StepSched sched = car_schedule<OBS>(p, parent, act, d, oLane);
+            WaveCull cull{~0u, true};   // the schedule covers the whole reach
+            if (!sched.valid) cull = car_cull<OBS>(p, ctl, d, obs);
+            if (__ballot(!car_theta_bounded(p, ctl, d)) != 0ull)   // rare: Payne-Hanek per lane
+                valid = car_euler_fast<OBS, true>(p, ctl, d, obs, cull, sched, out) && act;
+            else if (d.invAgentLength == 1.0f)
+                valid = car_euler_fast<OBS, false, true>(p, ctl, d, obs, cull, sched, out) && act;
+            else
+                valid = car_euler_fast<OBS, false>(p, ctl, d, obs, cull, sched, out) && act;
+        }
+    }
     if (act) {
-        Xorwow rs{ra.x, ra.y, ra.z, ra.w, rb.x, rb.y};
-        ChildOut out;
-        const bool valid = (AGENT == 0) ? propagate_car<OBS>(p, rs, d, obs, out)
-                                        : propagate_point<OBS>(p, rs, d, obs, out);
+        if (!fast)
+            valid = (AGENT == 0) ? propagate_car<OBS>(p, rs, d, obs, out) : propagate_point<OBS>(p, rs, d, obs, out);
         SBMP_STAMP(2);
-        const int r1 = getR1_k(out.state.x, out.state.y, d.R1Size, d.rcpR1Size, kN);   // N = 16 (KGMT.cu:8)
-        const int r2 = getR2_k(out.state.x, out.state.y, r1, d.R1Size, kN, d.R2Size, d.rcpR2Size, d.n);
+        int r1, r2;
+        bins_k(out.state.x, out.state.y, d, &r1, &r2);   // getR1 / getR2 (KGMT.cu:390-391), N = 16
         if (valid) {
             const float u = xorwow_uniform(rs);   // KGMT.cu:395
             if (r2 >= 0) {                        // r2 >= 0 implies r1 >= 0
@@ -1892,6 +1916,9 @@ __device__ __forceinline__ void step_planner(const KgmtDev& d, const ShardView& 
     }
 }
 
+#ifndef SBMP_VALU_DUP
+#define SBMP_VALU_DUP 0   // diagnostics: 1-4 run one part of the expanding wave twice (VALU attribution by PMC A/B)
+#endif
 // 5 waves per SIMD: the 1 + nBlocks workgroups (1,025 at 262,144 slots) fit the chip at once.
 // The expanding workgroups:
 //   prologue   RNG / count / control-block loads, then the child's controls (they need
@@ -2003,12 +2030,25 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) voi
     float4 oLane = make_float4(0.f, 0.f, 0.f, 0.f);
     if (AGENT == 0 && kRegObs > 0) oLane = G(d.obstacles)[lane % (kRegObs > 0 ? kRegObs : 1)];
     sR1P[tid] = 0;   // nR1 == kBlock
-    for (int i = tid; i < nW; i += kBlock) sNew[i] = 0u;
+    if (nW <= 2 * kBlock) {   // n <= 8 (uniform): two fixed stores, no loop
+        if (tid < nW) sNew[tid] = 0u;
+        if (tid + kBlock < nW) sNew[tid + kBlock] = 0u;
+    } else {
+        for (int i = tid; i < nW; i += kBlock) sNew[i] = 0u;
+    }
     // ---- the child's controls (statePropagator.cu:17-21) depend on the slot's stream
     // alone: drawn while the block counts are in flight (stored only for slots < S)
     Xorwow rs{ra.x, ra.y, ra.z, ra.w, rb.x, rb.y};
     ChildCtl ctl = draw_controls<AGENT>(rs, d);
     asm volatile("" : "+v"(ctl.a), "+v"(ctl.steer), "+v"(ctl.dur), "+v"(ctl.dt), "+v"(ctl.tanS));
+#if SBMP_VALU_DUP == 1   // diagnostics (VALU by part): the draw once more, on an opaque copy
+    {
+        Xorwow r2{ra.x, ra.y, ra.z, ra.w, rb.x, rb.y};
+        asm volatile("" : "+v"(r2.v0), "+v"(r2.v1), "+v"(r2.v2), "+v"(r2.v3), "+v"(r2.v4), "+v"(r2.d));
+        const ChildCtl c2 = draw_controls<AGENT>(r2, d);
+        asm volatile("" ::"v"(c2.a), "v"(c2.steer), "v"(c2.dur), "v"(c2.dt), "v"(c2.tanS), "v"(r2.v4), "v"(r2.d));
+    }
+#endif
     int A, jGoal;
     // the control block and the goal index were loaded per lane (vector loads do not
     // wait behind the scan's scalar work); the plan is wave-uniform, so scalar code
@@ -2151,11 +2191,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) voi
     const bool fromList = parent >= q.tsPrev;
     const int j = parent - q.tsPrev;
     const unsigned long long need = __ballot(fromList);
-    if (need) {
+    const int nS = SH ? sv.nRows : d.nBlocks;   // scan entries: blocks, or (sharded) rows
+    // the list block lo of this lane's position j (the wave's positions: `need`)
+    auto find_lo = [&](const int j, const bool fromList, const unsigned long long need) __attribute__((always_inline)) {
         const int jA = __builtin_amdgcn_readlane(j, (int)__builtin_ctzll(need));
         const int jB = __builtin_amdgcn_readlane(j, 63 - (int)__builtin_clzll(need));
         int lo = 0;
-        const int nS = SH ? sv.nRows : d.nBlocks;   // scan entries: blocks, or (sharded) rows
         if (jB - jA <= 1) {
             const int jj = (lane < 32) ? jA : jB;
             const int sub = lane & 31;
@@ -2180,6 +2221,17 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) voi
             if (fromList)
                 while (lo + 1 < nS && sPfx[lo + 1] <= j) ++lo;
         }
+        return lo;
+    };
+    if (need) {
+        const int lo = find_lo(j, fromList, need);
+#if SBMP_VALU_DUP == 2   // diagnostics (VALU by part): the search once more, on opaque copies
+        {
+            int j2 = j;
+            asm volatile("" : "+v"(j2));
+            asm volatile("" ::"v"(find_lo(j2, fromList, need)));
+        }
+#endif
         if (fromList) {
             if constexpr (SH) {   // the row's blocks: from the LDS table (round 4: one more L2 round trip)
                 int blk, idx;
@@ -2243,6 +2295,15 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) voi
         if (fast) {
             // a huge steering tan can drive theta past Cody-Waite's range within a child
             const StepSched sched = car_schedule<OBS>(p, parent, act, d, oLane);
+#if SBMP_VALU_DUP == 3   // diagnostics: the schedule and the theta bound once more, on opaque copies
+            {
+                float4 p2 = p;
+                asm volatile("" : "+v"(p2.x), "+v"(p2.y), "+v"(p2.z), "+v"(p2.w));
+                const StepSched s2 = car_schedule<OBS>(p2, parent, act, d, oLane);
+                const unsigned long long tb = __ballot(!car_theta_bounded(p2, ctl, d));
+                asm volatile("" ::"s"(s2.boxes), "s"(s2.bounds), "s"(tb));
+            }
+#endif
             WaveCull cull{~0u, true};   // the schedule covers the whole reach
             if (!sched.valid) cull = car_cull<OBS>(p, ctl, d, obs);
             if (__ballot(!car_theta_bounded(p, ctl, d)) != 0ull)   // rare: Payne-Hanek per lane
@@ -2265,6 +2326,15 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) voi
     // ---- bins (KGMT.cu:390-391) and the accept test (KGMT.cu:394-411, D2)
     int q1 = -1, q2 = -1;
     if (act) bins_k(out.state.x, out.state.y, d, &q1, &q2);   // N = 16 (KGMT.cu:8)
+#if SBMP_VALU_DUP == 4   // diagnostics: the binning once more, on opaque copies
+    if (act) {
+        float x2 = out.state.x, y2 = out.state.y;
+        asm volatile("" : "+v"(x2), "+v"(y2));
+        int a2, b2;
+        bins_k(x2, y2, d, &a2, &b2);
+        asm volatile("" ::"v"(a2), "v"(b2));
+    }
+#endif
     // The planner workgroup publishes iteration t's scores and snapshot as 8-B words
     // tagged with t (step_planner); each lane that takes the test reads its two words
     // from L2 now, and the stores below overlap that round trip.  q2 >= 0 implies q1 >= 0.
@@ -2339,7 +2409,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) voi
         ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)(word >> 32), 0) << 32) |
         (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)word, 0);
     const unsigned long long wordAll = word0 | mask;   // GNew |= accept (stale bits survive)
-    const bool flagged = (wordAll >> lane) & 1ull;
+    const bool flagged = __builtin_amdgcn_inverse_ballot_w64(wordAll);   // this lane's bit of wordAll (a lane mask)
     if ((wordAll & ~__ballot(act)) != 0ull) {   // rare; keeps the wait below off the common path
         if (flagged && !act) {   // a stale flag on a slot past S: the child last written there
             cs = G(d.uState)[slot];
@@ -2395,7 +2465,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) voi
             __builtin_amdgcn_raw_buffer_store_b128(sbmp_u32x4{__float_as_uint(cc.x), __float_as_uint(cc.y), __float_as_uint(cc.z), __float_as_uint(cc.w)}, rl, vo + 16, so, 0);
             __builtin_amdgcn_raw_buffer_store_b128(sbmp_u32x4{__float_as_uint(cost), 0u, 0u, 0u}, rl, vo + 32, so, 0);
 #else
-            const int e = (cp * d.nBlocks * kBlock + b * kBlock + waveOff + idxW) * kStepEntry;   // < 2^27 entries
+            // < 2^27 entries; the row part is uniform, the lane part a 24-bit multiply (full rate)
+            const int e = (cp * d.nBlocks + b) * kBlock * kStepEntry + (int)__umul24((unsigned)(waveOff + idxW), (unsigned)kStepEntry);
             store_wt(d.stepList, e, cs);
             store_wt(d.stepList, e + 1, cc);
             store_wt(d.stepList, e + 2, make_float4(cost, 0.0f, 0.0f, 0.0f));
@@ -2423,9 +2494,15 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) voi
         // replicas: a device atomic on one word serialises (~11 ns each); in the early
         // iterations most blocks set the same few words, so each replica sees 1/kNewReps
         SBMP_GAS uint32_t* const newCur = G(d.stepR2New) + ((size_t)(t % 3) * kNewReps + (size_t)(b % kNewReps)) * nW;
-        for (int i = tid; i < nW; i += kBlock) {
-            const uint32_t w = sNew[i];
-            if (w) __hip_atomic_fetch_or(newCur + i, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (nW <= 2 * kBlock) {   // n <= 8 (uniform): both words' LDS reads, then their atomics
+            const uint32_t w0 = tid < nW ? sNew[tid] : 0u, w1 = tid + kBlock < nW ? sNew[tid + kBlock] : 0u;
+            if (w0) __hip_atomic_fetch_or(newCur + tid, w0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (w1) __hip_atomic_fetch_or(newCur + tid + kBlock, w1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+            for (int i = tid; i < nW; i += kBlock) {
+                const uint32_t w = sNew[i];
+                if (w) __hip_atomic_fetch_or(newCur + i, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
         }
     }
     if (tid == 0) {   // the block's flagged count and its lowest goal child (in-block index)

@@ -59,3 +59,16 @@ def test_scanner_catches_the_round3_store_form(tmp_path):
     _, _, hazards = isa_hazards.scan_library(so)
     assert hazards, "the SGPR-soffset list stores compiled without a hazard: the demo no longer reproduces it"
     assert all("buffer_store_dwordx4" in s for s, _ in hazards)
+
+
+def test_hot_kernels_use_no_scratch():
+    """Every k_step and k_expand instantiation keeps its state in registers: no scratch
+    (private segment) and no VGPR spills.  Round 6: indexing the register obstacle list by
+    lane put it in scratch and made k_expand 25% slower."""
+    if not os.path.exists(LIB):
+        pytest.skip("libsbmp.so not built (python -m cudasbmp_amd.build)")
+    res = isa_hazards.kernel_resources(LIB)
+    hot = {k: v for k, v in res.items() if "k_step" in k or "k_expand" in k}
+    assert len(hot) >= 40, sorted(res)[:8]
+    bad = {k: v for k, v in hot.items() if v[1] or v[2]}
+    assert not bad, f"{len(bad)} hot kernels spill or use scratch: {list(bad.items())[:4]}"

@@ -112,6 +112,24 @@ def scan_library(lib: str):
         return len(cos), stores, hazards
 
 
+def kernel_resources(lib: str):
+    """{kernel symbol: (vgpr_count, sgpr spill count, private segment bytes)} from the
+    code objects' metadata notes."""
+    out = {}
+    with tempfile.TemporaryDirectory() as tmp:
+        for co in code_objects(lib, tmp):
+            notes = subprocess.run([f"{LLVM}/llvm-readelf", "--notes", co], check=True, capture_output=True,
+                                   text=True).stdout
+            for b in notes.split("- .agpr_count")[1:]:
+                name = re.search(r"\.name:\s+(\S+)", b)
+                vgpr = re.search(r"\.vgpr_count:\s+(\d+)", b)
+                priv = re.search(r"\.private_segment_fixed_size:\s+(\d+)", b)
+                vsp = re.search(r"\.vgpr_spill_count:\s+(\d+)", b)
+                if name and vgpr and priv:
+                    out[name.group(1)] = (int(vgpr.group(1)), int(vsp.group(1)) if vsp else 0, int(priv.group(1)))
+    return out
+
+
 def main():
     lib = sys.argv[1] if len(sys.argv) > 1 else os.path.join(os.path.dirname(__file__), "..", "cudasbmp_amd",
                                                               "libsbmp.so")
