@@ -422,17 +422,21 @@ __device__ __forceinline__ void batch_rule(const KgmtDev& d, int treeSize, int n
     *k = 0;
     *nExp = 0;
     if (nG <= 0) return;   // D7: a zero-block launch is a no-op
-    long long remaining = (long long)d.M - treeSize;
+    // Both callers run it only while treeSize < M (KGMT.cu:255), so the room left is in
+    // [1, M - 1] and everything below is 32-bit scalar arithmetic (gfx9's scalar unit has
+    // no 64-bit ordered compare: the 64-bit form went through VALU compares and moves on
+    // the plan's critical path, which every expanding wave waits for).
+    int remaining = d.M - treeSize;
     if (d.cap > 0 && remaining > d.cap) remaining = d.cap;
     if (d.cap > 0 && d.batchRule == 1) {   // D14: fill the batch
-        if (nG <= remaining) {   // 1 <= remaining <= M - 1 < 2^31: a 32-bit quotient
-            *k = (remaining < kFastDivMax) ? div_small((int)remaining, nG) : (int)remaining / nG;
+        if (nG <= remaining) {
+            *k = (remaining < kFastDivMax) ? div_small(remaining, nG) : remaining / nG;
             *nExp = nG;
         } else {
             *k = 1;
-            *nExp = (int)remaining;
+            *nExp = remaining;
         }
-    } else if (32ll * nG <= remaining) {
+    } else if (nG <= (remaining >> 5)) {   // 32 nG <= remaining, exactly (remaining >= 0)
         *k = 32;
         *nExp = nG;
     } else {
@@ -1651,7 +1655,7 @@ __device__ __forceinline__ StepPlan step_plan(const KgmtDev& d, int t, int expan
     // The lowest inserted row of t-1 inside the goal radius (D4): rows grow with j,
     // so if the lowest candidate is not inserted (D13) none is.
     q.newGoal = goalIdx;
-    if (jGoal < q.nIns && (long long)q.tsPrev + jGoal < d.M) q.newGoal = min(q.newGoal, q.tsPrev + jGoal);
+    if (jGoal < q.nIns && jGoal < d.M - q.tsPrev) q.newGoal = min(q.newGoal, q.tsPrev + jGoal);   // tsPrev <= M: no overflow
     q.runT = (t <= d.numIterations) && (q.treeSize < d.M);   // KGMT.cu:118,255
     q.nG = 0;
     q.k = 0;
@@ -1921,9 +1925,10 @@ __device__ __forceinline__ void step_planner(const KgmtDev& d, const ShardView& 
 #endif
 // 5 waves per SIMD: the 1 + nBlocks workgroups (1,025 at 262,144 slots) fit the chip at once.
 // The expanding workgroups:
-//   prologue   RNG / count / control-block loads, then the child's controls (they need
-//              the slot's stream only) while the counts are in flight; the count scan,
-//              the plan scalars, the D6 clear, the parent (list search);
+//   prologue   RNG / count / control-block loads; the count scan; the plan scalars
+//              (wave 0) while waves 1-3 draw the child's controls (they need the slot's
+//              stream only; wave 0 draws after the plan's barrier); the D6 clear, the
+//              parent (list search);
 //   propagate  the Euler loop (statePropagator.cu:23-65);
 //   accept     each lane reads the two published words it needs (score of its R1 cell,
 //              snapshot word of its R2 cell, tagged with t) straight from L2, with no
@@ -2037,10 +2042,17 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) voi
         for (int i = tid; i < nW; i += kBlock) sNew[i] = 0u;
     }
     // ---- the child's controls (statePropagator.cu:17-21) depend on the slot's stream
-    // alone: drawn while the block counts are in flight (stored only for slots < S)
+    // alone.  Drawn after the count scan (round 6): waves 1-3 while wave 0 plans, wave 0
+    // right after the plan's barrier.  Drawn before the scan (rounds 3-5) they held the
+    // scan behind the XORWOW states' arrival, the launch's 6.3 MB burst, although the
+    // 4-KB counts arrive first: count scan done 2.02 -> 1.32 us p50, every later phase
+    // ~0.55 us earlier (profiles/r06/prologue/).
     Xorwow rs{ra.x, ra.y, ra.z, ra.w, rb.x, rb.y};
-    ChildCtl ctl = draw_controls<AGENT>(rs, d);
-    asm volatile("" : "+v"(ctl.a), "+v"(ctl.steer), "+v"(ctl.dur), "+v"(ctl.dt), "+v"(ctl.tanS));
+    ChildCtl ctl;
+    auto draw = [&]() __attribute__((always_inline)) {
+        ctl = draw_controls<AGENT>(rs, d);
+        asm volatile("" : "+v"(ctl.a), "+v"(ctl.steer), "+v"(ctl.dur), "+v"(ctl.dt), "+v"(ctl.tanS));
+    };
 #if SBMP_VALU_DUP == 1   // diagnostics (VALU by part): the draw once more, on an opaque copy
     {
         Xorwow r2{ra.x, ra.y, ra.z, ra.w, rb.x, rb.y};
@@ -2087,7 +2099,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) voi
                 sWaveDiv[lane] = make_int2(g0, s0 - g0 * q0.k);
             }
         }
+        else {   // waves 1-3 draw their controls while wave 0 plans
+            draw();
+        }
         __syncthreads();
+        if (wave == 0) draw();
         q = uniform_plan(sPlan);
 #ifdef SBMP_TL_PROLOGUE   // diagnostics: stamp 4 = after the plan's barrier (instead of the hand-off)
         SBMP_STAMP(4);
