@@ -739,6 +739,119 @@ __device__ void insert_block(const KgmtDev& d, int t, int gblock, long long* st)
     }
 }
 
+// The same for iterations of more than 1,024 blocks (the two-launch form at c4 / c5's
+// 1,048,576 children): insert workgroup w0 takes blocks w0 + r G (r < kInsertMaxR; G a
+// multiple of 8, so every one of them ran on this workgroup's XCD in k_expand, whose
+// L2 holds its slots) and reduces the block counts once for all of them.  One workgroup
+// per block (insert_block) dispatched 4,096 workgroups that each re-read the 16-KB
+// count array: k_finish 12.4 us at c4's 1,048,576 children, its insert workgroups
+// entering over 8 us (profiles/r05/workloads/k_finish_c4_1M_iter20.txt).
+#ifndef SBMP_INSERT_R
+#define SBMP_INSERT_R 4
+#endif
+constexpr int kInsertMaxR = SBMP_INSERT_R;
+__device__ void insert_blocks(const KgmtDev& d, int t, int w0, int G, long long* st) {
+    __shared__ int sRed[kInsertMaxR + 1][kBlock / kWave];
+    __shared__ int sWaveCnt[kInsertMaxR][kBlock / kWave];
+    const int lane = threadIdx.x & (kWave - 1);
+    const int wave = threadIdx.x >> 6;
+    // every load that depends on nothing else first: the flag words, the control
+    // block, the block counts
+    int gb[kInsertMaxR];
+    unsigned long long word[kInsertMaxR];
+#pragma unroll
+    for (int r = 0; r < kInsertMaxR; ++r) {
+        gb[r] = w0 + r * G;
+        word[r] = (gb[r] < d.nBlocks) ? d.gnewIn[gb[r] * (kBlock / kWave) + wave] : 0ull;
+    }
+    const IterCtrl c = d.ctrl[t];
+    const int nb4 = (d.nBlocks + 3) & ~3;
+    int p[kInsertMaxR] = {}, tot = 0;
+#pragma unroll 4
+    for (int i = (int)threadIdx.x * 4; i < nb4; i += kBlock * 4) {
+        const int4 v = *reinterpret_cast<const int4*>(d.blockCountIn + i);
+        const int e[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            tot += e[k];
+#pragma unroll
+            for (int r = 0; r < kInsertMaxR; ++r) p[r] += (i + k < gb[r]) ? e[k] : 0;
+        }
+    }
+    if (!c.executed) return;   // uniform
+    SBMP_FIN_STAMP(1);
+    // the flagged lanes' children, in flight while the prefixes are reduced
+    float4 us[kInsertMaxR], uc[kInsertMaxR];
+    bool flagged[kInsertMaxR];
+#pragma unroll
+    for (int r = 0; r < kInsertMaxR; ++r) {
+        if (gb[r] >= d.nBlocks || gb[r] * kBlock >= c.H) word[r] = 0ull;   // uniform: never ran
+        flagged[r] = (word[r] >> lane) & 1ull;
+        us[r] = uc[r] = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (flagged[r]) {
+            const int slot = gb[r] * kBlock + (int)threadIdx.x;
+            us[r] = d.uState[slot];
+            uc[r] = d.uCtrl[slot];
+        }
+    }
+    tot = wave_sum(tot);
+#pragma unroll
+    for (int r = 0; r < kInsertMaxR; ++r) p[r] = wave_sum(p[r]);
+    if (lane == 0) {
+#pragma unroll
+        for (int r = 0; r < kInsertMaxR; ++r) {
+            sRed[r][wave] = p[r];
+            sWaveCnt[r][wave] = __popcll(word[r]);
+        }
+        sRed[kInsertMaxR][wave] = tot;
+    }
+    __syncthreads();
+    const int A = sRed[kInsertMaxR][0] + sRed[kInsertMaxR][1] + sRed[kInsertMaxR][2] + sRed[kInsertMaxR][3];
+    SBMP_FIN_STAMP(2);
+    const int m32 = d.M / 32;
+    const int grid = min(A, m32);   // updateG launch: min(|GNew|, M/32) blocks of 32 (KGMT.cu:231)
+    const int nIns = 32 * grid < A ? 32 * grid : A;
+    const long long cleared = d.fixGNewClear ? (1ll << 62) : 32ll * grid;
+#pragma unroll
+    for (int r = 0; r < kInsertMaxR; ++r) {
+        if (word[r] == 0ull) continue;   // uniform
+        int waveOff = sRed[r][0] + sRed[r][1] + sRed[r][2] + sRed[r][3];
+        for (int i = 0; i < wave; ++i) waveOff += sWaveCnt[r][i];
+        if (flagged[r]) {
+            const int j = waveOff + __popcll(word[r] & ((1ull << lane) - 1ull));
+            const int dst = c.treeSize + j;
+            if (j < nIns && dst < d.M) {   // D13: the reference writes past M here
+                const int parent = __float_as_int(uc[r].w);
+                const float cost = d.treeCtrl[parent].w + uc[r].z;   // getCost = duration (KGMT.cu:631-633)
+                d.treeState[dst] = us[r];
+                d.treeCtrl[dst] = make_float4(uc[r].x, uc[r].y, uc[r].z, cost);
+                d.treeParent[dst] = parent;
+                const float dx = us[r].x - d.goalX, dy = us[r].y - d.goalY;   // inGoalRegion, KGMT.cu:635-638
+                const float d2 = dx * dx + dy * dy;
+                if (__builtin_sqrtf(d2) < d.goalThreshold) atomicMin(&d.status->goalIdx, dst);
+            }
+        }
+        if (lane == 0) {   // D6: only GNew[0 .. 32*grid) is cleared
+            const int w = gb[r] * (kBlock / kWave) + wave;
+            const long long base = (long long)w * kWave;
+            unsigned long long nw_ = word[r];
+            if (base + kWave <= cleared) nw_ = 0ull;
+            else if (base < cleared) nw_ = word[r] & ~((1ull << (cleared - base)) - 1ull);
+            if (nw_ != word[r]) d.gnewIn[w] = nw_;
+        }
+    }
+    SBMP_FIN_STAMP(3);
+}
+
+// k_finish's insert workgroups for an iteration of nBlocks 256-slot blocks: one per
+// block up to 1,024 blocks, else the fewest (a multiple of 8) that give each at most
+// kInsertMaxR.
+int finish_insert_groups(int nBlocks) {
+    if (nBlocks <= 1024) return nBlocks;
+    const int g = (nBlocks + kInsertMaxR - 1) / kInsertMaxR;
+    return (g + 7) & ~7;
+}
+
 // Sharded ranks: iteration t's accepted (and stale, D6) children of
 // every rank, record-driven.  The owners' record lists, concatenated in rank order,
 // are walked with a grid-stride loop; record (block g, index i) becomes row
@@ -879,7 +992,9 @@ __global__ __launch_bounds__(kBlock) void k_finish(KgmtDev d, int t) {
         insert_records(d, t, (int)blockIdx.x - 1, (int)gridDim.x - 1, tl ? st : nullptr);
         owner_clear(d, t, (int)blockIdx.x - 1);
     } else if (blockIdx.x >= kInsertBase) {   // blocks 1 .. kInsertBase-1 are idle
-        insert_block(d, t, (int)blockIdx.x - kInsertBase, tl ? st : nullptr);
+        const int G = (int)gridDim.x - kInsertBase;
+        if (G >= d.nBlocks) insert_block(d, t, (int)blockIdx.x - kInsertBase, tl ? st : nullptr);
+        else insert_blocks(d, t, (int)blockIdx.x - kInsertBase, G, tl ? st : nullptr);
     }
     if (tl) {
         st[7] = (long long)__builtin_amdgcn_s_memrealtime();

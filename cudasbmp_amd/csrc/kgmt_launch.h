@@ -36,6 +36,7 @@ int step_resident_groups(const KgmtDev& d, int agent, int variant, StepResidency
 void launch_fold_r2(const KgmtDev& d, int tFirst, int tLast, hipStream_t s, const KernelTiming& tm = KernelTiming());
 // k_finish(t): insert iteration t (insertBlocks = every global 256-slot block) +
 // prepare iteration t+1.  t = 0 prepares iteration 1 only (insertBlocks = 0).
+int finish_insert_groups(int nBlocks);   // k_finish's insert workgroups for nBlocks 256-slot blocks
 void launch_finish(const KgmtDev& d, int t, int insertBlocks, hipStream_t s,
                    const KernelTiming& tm = KernelTiming());
 // Sharded ranks: pack this rank's accepted children of iteration t (blocks = owned blocks).

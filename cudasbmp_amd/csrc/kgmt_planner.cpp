@@ -886,9 +886,11 @@ void KgmtPlanner::flush() {
 }
 
 void KgmtPlanner::stage_finish(int t) {
-    // single rank: one insert block per 256-slot block; sharded: the record-driven
-    // insert and the owner's GNew clear, one block per owned block
-    launch_finish(d_, t, d_.sharded ? expandBlocks_ : kInsertBase - 1 + d_.nBlocks, stream_, timing(K_FINISH));
+    // single rank: one insert workgroup per 256-slot block up to 1,024 blocks, then up to
+    // kInsertMaxR blocks each (insert_blocks); sharded: the record-driven insert and the
+    // owner's GNew clear, one workgroup per owned block
+    launch_finish(d_, t, d_.sharded ? expandBlocks_ : kInsertBase - 1 + finish_insert_groups(d_.nBlocks), stream_,
+                  timing(K_FINISH));
 }
 
 void KgmtPlanner::stage_fold(int t) {

@@ -107,6 +107,19 @@ def test_c4_local_group_8_ranks_1M_bit_exact(obstacles, oracle_lib):
     assert_same_state(g, o, label="c4 8-rank local group")
 
 
+@pytest.mark.parametrize("blocks,clear", [(1031, True), (2049, False)])
+def test_two_launch_grouped_inserts_ragged_bit_exact(blocks, clear, obstacles, oracle_lib):
+    """Above 1,024 blocks k_finish's insert workgroups take up to 4 blocks each at a
+    stride of the group count (insert_blocks): 1,031 blocks (264 groups, the last blocks
+    of the stride past the end) and 2,049 blocks (520 groups) with the reference's
+    partial GNew clear (D6), whole state bit-exact."""
+    g, o, r = _run(_bench_kw(256 * blocks, 6, maxTreeSize=1 << 23, fixGNewClear=clear), BENCH_SEED, obstacles)
+    info = g.path_info()
+    assert info["form"] == "two-launch", info
+    assert g.iter_log()[:, 5].max() == 256 * blocks
+    assert_same_state(g, o, label=f"two-launch, {blocks} blocks")
+
+
 def test_c5_1M_bit_exact(oracle_lib):
     obs = _c5_obstacles()
     assert len(obs) == 10000
