@@ -671,6 +671,16 @@ __device__ __forceinline__ bool motion_valid_culled(float minx, float miny, floa
 #define SBMP_GRID_BATCH 8
 #endif
 constexpr int kGridBatch = SBMP_GRID_BATCH;   // boxes loaded per round trip; also the padding rows of gridBoxes
+// k_expand (the global cell-start table, 4-5 waves per SIMD) tests 4 rows per batch: fewer
+// rows past the cell run for the VALU, where its occupancy hides the extra round trips
+// (c5 at 1,048,576 children: k_expand 95.5 -> 85.3 us); k_step (the LDS table, 2 waves per
+// SIMD at c5's per-rank shape, latency-bound) keeps 8 (4 cost it 1%; 16 spills).
+// profiles/r06/workloads/grid_batch/.
+#ifndef SBMP_GRID_BATCH_GLOBAL
+#define SBMP_GRID_BATCH_GLOBAL 4
+#endif
+constexpr int kGridBatchGlobal = SBMP_GRID_BATCH_GLOBAL;
+static_assert(kGridBatchGlobal <= kGridBatch, "the padding rows cover the larger batch");
 
 // The segment's cell span and the start offsets of its first two cell rows (grid_run_sep
 // tests their boxes).
@@ -702,7 +712,7 @@ __device__ __forceinline__ GridRun grid_run(float minx, float miny, float maxx, 
 }
 
 // min over the span's boxes of the separation metric (< 0: a box overlaps the segment box).
-template <class SP>
+template <int B, class SP>
 __device__ __forceinline__ float grid_run_sep(GridRun q, float minx, float miny, float maxx, float maxy,
                                               const KgmtDev& d, SP start) {
     const SBMP_GAS float4* const boxes = G(d.gridBoxes);
@@ -720,13 +730,13 @@ __device__ __forceinline__ float grid_run_sep(GridRun q, float minx, float miny,
 #pragma unroll
         for (int r = 0; r < 2; ++r) {
             const int b = r ? q.b1 : q.b0, e = r ? q.e1 : q.e0;
-            for (int i = b; i < e && !(sep < 0.0f); i += kGridBatch) {
+            for (int i = b; i < e && !(sep < 0.0f); i += B) {
                 const SBMP_GAS float4* const row = boxes + i;
-                float4 o[kGridBatch];
+                float4 o[B];
 #pragma unroll
-                for (int k = 0; k < kGridBatch; ++k) o[k] = row[k];
+                for (int k = 0; k < B; ++k) o[k] = row[k];
 #pragma unroll
-                for (int k = 0; k < kGridBatch; ++k) {
+                for (int k = 0; k < B; ++k) {
                     const sbmp_f32x2 lo = sbmp_f32x2{o[k].x, o[k].y} - mx;
                     const sbmp_f32x2 hi = mn - sbmp_f32x2{o[k].z, o[k].w};
                     const float sk = __builtin_fmaxf(vmax3(lo.x, lo.y, hi.x), hi.y);
@@ -742,18 +752,18 @@ __device__ __forceinline__ float grid_run_sep(GridRun q, float minx, float miny,
     return sep;
 }
 
-template <class SP>
+template <int B, class SP>
 __device__ __forceinline__ bool grid_free_fast(float minx, float miny, float maxx, float maxy, const KgmtDev& d,
                                                SP start) {
-    return !(grid_run_sep(grid_run(minx, miny, maxx, maxy, d, start), minx, miny, maxx, maxy, d, start) < 0.0f);
+    return !(grid_run_sep<B>(grid_run(minx, miny, maxx, maxy, d, start), minx, miny, maxx, maxy, d, start) < 0.0f);
 }
 // the table the grid query reads: LDS when the caller staged it (sStart != nullptr is
 // decided at compile time by LDSG), else global memory
 template <bool LDSG>
 __device__ __forceinline__ bool grid_free_at(float minx, float miny, float maxx, float maxy, const KgmtDev& d,
                                              const int* sStart) {
-    if constexpr (LDSG) return grid_free_fast(minx, miny, maxx, maxy, d, (const SBMP_LDS int*)sStart);
-    else return grid_free_fast(minx, miny, maxx, maxy, d, G(d.gridStart));
+    if constexpr (LDSG) return grid_free_fast<kGridBatch>(minx, miny, maxx, maxy, d, (const SBMP_LDS int*)sStart);
+    else return grid_free_fast<kGridBatchGlobal>(minx, miny, maxx, maxy, d, G(d.gridStart));
 }
 
 // reference statePropagator.cu:5-76 (car).  Same operation sequence as the oracle
